@@ -1,0 +1,122 @@
+/*
+ * mpcracing.h -- C ABI of the MI355X batched racing-MPC solver (libmpcracing.so).
+ *
+ * Drop-in boundary for the reference's hot path: the reference has no FFI; its
+ * boundary is the Python class control.MPC.MPC (AlexGisi/mpc-racing
+ * control/MPC.py:10-22 constructor, :183-184 solution()).  Each entry point
+ * below replaces a piece of that class:
+ *
+ *   mr_config_default / mr_create   <- FixedControllerParameters (control/ControllerParameters.py:3-23),
+ *                                      VehicleParameters (models/VehicleParameters.py:3-41),
+ *                                      the IPOPT options dict (control/MPC.py:151-161)
+ *   mr_set_tyres                    <- learned Pacejka tyres substituted into f_vehicle
+ *                                      (learning/vehicle.py:79-92, :155-160)
+ *   mr_solve_batch                  <- MPC.__init__ build + opti.solve() + the ret tuple
+ *                                      (control/MPC.py:30-181) for B independent instances
+ *   mr_last_error                   <- the RuntimeError text printed at control/MPC.py:173
+ *
+ * Conventions: every function returns 0 on success and a negative code on error
+ * (message via mr_last_error(), thread-local).  All batch arrays are caller-owned
+ * DEVICE pointers (e.g. torch tensors' data_ptr()) in structure-of-arrays layout
+ * with the instance index fastest: element [c][i] of a [C][B] array is at
+ * ptr[c*B + i].  All I/O is float64 regardless of the handle's compute precision.
+ * Calls are ordered on the given HIP stream; a handle is bound to one device and is
+ * not thread-safe.
+ */
+#ifndef MPCRACING_H
+#define MPCRACING_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MR_OK 0
+#define MR_ERR_ARG (-1)
+#define MR_ERR_HIP (-2)
+#define MR_ERR_STATE (-3)
+
+/* dynamics models of the NLP */
+#define MR_MODEL_KINEMATIC 0       /* control/MPC.py:231-260 (f_vehicle_kinematic)          */
+#define MR_MODEL_DYNAMIC 1         /* control/MPC.py:186-229 (f_vehicle, the reference NLP)  */
+#define MR_MODEL_BLENDED 2         /* lambda*dyn + (1-lambda)*kin, models/BlendedBicycleModel.py:22-46 */
+#define MR_MODEL_BLENDED_PACEJKA 3 /* blended with learned Pacejka lateral forces            */
+#define MR_MODEL_DYNAMIC_PACEJKA 4 /* dynamic with learned Pacejka lateral forces            */
+
+#define MR_PREC_FP64 0
+#define MR_PREC_FP32 1
+
+/* per-instance solver status (replaces the try/except + breakpoint() of control/MPC.py:164-181) */
+#define MR_STATUS_SOLVED 0
+#define MR_STATUS_ACCEPTABLE 1
+#define MR_STATUS_MAX_ITER 2
+#define MR_STATUS_FAILED 3 /* non-finite values or no inertia-correct factorisation */
+#define MR_STATUS_LANE_INFEASIBLE 4 /* converged, but a lane row needed its elastic slack (> 1e-6 m):
+                                       the hard-constrained NLP is locally infeasible */
+
+typedef struct mr_config {
+  int32_t N;           /* horizon (FixedControllerParameters.N = 30 unless the caller passes N) */
+  int32_t model;       /* MR_MODEL_* */
+  int32_t precision;   /* MR_PREC_* : arithmetic type of the solve */
+  int32_t lane_bounds; /* 1 enables |e_C(S_i, X_i)| <= max_error, i = 1..N (the commented MPC.py:135) */
+  int32_t max_batch;   /* workspace capacity (instances) */
+  int32_t device;      /* HIP device ordinal */
+  int32_t max_iter;    /* FixedControllerParameters.max_iter = 500 */
+  int32_t acceptable_iter; /* IPOPT acceptable_iter (15); 0 disables acceptable termination */
+  double Ts;           /* sampling time */
+  double tol;          /* KKT tolerance of the scaled NLP (IPOPT tol) */
+  double acceptable_tol;
+  double lane_penalty; /* exact-penalty weight of the elastic lane rows (cost per metre of violation) */
+  /* FixedControllerParameters (control/ControllerParameters.py:3-23) */
+  double lambda_s, alpha_L, min_steer, max_steer, min_throttle, max_steer_delta, min_steer_delta,
+      max_throttle_delta, min_throttle_delta, q_v_max, v_max, min_s_delta;
+  /* VehicleParameters (models/VehicleParameters.py:3-41); max_steer_deg = VehicleParameters.max_steer */
+  double m, Iz, lf, lr, Cf, Cr, T_max, r_wheel, C_wheel, R, rho, C_d, A_f, C_roll, g, max_steer_deg,
+      Vblendmin, Vblendmax;
+} mr_config;
+
+typedef struct mr_inputs {
+  const double* state0;  /* [8][B]: x, y, yaw, v_x, v_y, yaw_dot, throttle, steer (NaN = None) */
+  const double* s0;      /* [B] initial progress */
+  const double* cx;      /* [5][B] centerline x polynomial, highest order first, global s */
+  const double* cy;      /* [5][B] */
+  const double* max_error; /* [B] lane half width (used when lane_bounds) */
+  const double* runtime; /* [5][B] RuntimeControllerParameters: alpha_c, d_max, q_v_y, n, beta_delta.
+                            NOTE control/MPC.py:50 reads the CLASS attribute d_max; the Python
+                            drop-in passes that value here to keep the quirk. */
+  const double* u_init;  /* optional [2][N][B] initial controls (already shifted last_controls,
+                            control/MPC.py:120-125); NULL -> (throttle0, steer0) repeated */
+} mr_inputs;
+
+typedef struct mr_outputs {
+  double* X;      /* [6][N+1][B] States (control/MPC.py:166) */
+  double* U;      /* [2][N][B] */
+  double* S;      /* [N+1][B] S_hat */
+  double* eC;     /* [N][B] e_hat_C(S_hat[i], States[:, i]), i = 0..N-1 */
+  double* eL;     /* [N][B] e_hat_L */
+  int32_t* status; /* [B] MR_STATUS_* */
+  int32_t* iters;  /* [B] interior-point iterations */
+  double* obj;     /* optional [B] objective value (NULL to skip) */
+  double* kkt;     /* optional [B] final scaled KKT error (NULL to skip) */
+} mr_outputs;
+
+typedef struct mr_handle mr_handle;
+
+int mr_version(void);
+const char* mr_last_error(void);
+int mr_config_default(mr_config* cfg);
+int mr_create(mr_handle** h, const mr_config* cfg);
+int mr_destroy(mr_handle* h);
+/* Pacejka coefficients a[0..8] and vertical load Fz for the front and back tyre
+   (state dict keys front_tire.a / front_tire.Fz / back_tire.a / back_tire.Fz). */
+int mr_set_tyres(mr_handle* h, const double* a_front, double Fz_front, const double* a_back, double Fz_back);
+int mr_solve_batch(mr_handle* h, int32_t B, const mr_inputs* in, mr_outputs* out, void* hip_stream);
+/* workspace bytes used per instance for the handle's configuration */
+int64_t mr_workspace_bytes_per_instance(const mr_handle* h);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MPCRACING_H */

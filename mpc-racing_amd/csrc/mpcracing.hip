@@ -1,0 +1,152 @@
+// libmpcracing.so -- gfx950 batched racing-MPC solver and its C ABI (include/mpcracing.h).
+//
+// One thread per MPC instance runs the whole interior-point solve (mr_solver.h);
+// the per-stage working set lives in an HBM workspace in structure-of-arrays layout
+// [stage][field][instance] so every load/store of a wavefront is one coalesced
+// 64 x sizeof(T) segment.  Instances are independent, so there is no inter-thread
+// communication and a launch needs no synchronisation besides its end.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+#include <string>
+
+#include "mr_batch.h"
+
+using namespace mr;
+
+struct mr_handle {
+  mr_config cfg;
+  void* ws;
+  size_t ws_bytes;
+  int64_t ws_stride;
+  TyreCoef<double> tf, tr;
+  int have_tyres;
+};
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(x)                                                                  \
+  do {                                                                              \
+    hipError_t e_ = (x);                                                            \
+    if (e_ != hipSuccess) return fail(MR_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+constexpr int kBlock = 64;
+
+template <typename T, int MODEL>
+__global__ __launch_bounds__(kBlock) void mr_solve_kernel(ProbParams<T> P, mr_inputs in, mr_outputs out, int B,
+                                                          T* ws, int64_t stride) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= B) return;
+  WS<T> W{ws + i, stride};
+  solve_instance<T, MODEL>(P, in, out, B, i, W);
+}
+
+template <typename T>
+static size_t elem_size() { return sizeof(T); }
+
+static size_t ws_bytes_per_instance(const mr_config& c) {
+  const size_t per = (size_t)WF::NF * (size_t)(c.N + 1);
+  return per * (c.precision == MR_PREC_FP32 ? sizeof(float) : sizeof(double));
+}
+
+template <typename T, int MODEL>
+static int launch(mr_handle* h, int B, const mr_inputs* in, mr_outputs* out, hipStream_t st) {
+  ProbParams<T> P;
+  fill_params<T>(h->cfg, h->tf, h->tr, P);
+  dim3 grid((B + kBlock - 1) / kBlock), block(kBlock);
+  hipLaunchKernelGGL((mr_solve_kernel<T, MODEL>), grid, block, 0, st, P, *in, *out, B, (T*)h->ws, h->ws_stride);
+  HIP_TRY(hipGetLastError());
+  return MR_OK;
+}
+
+template <typename T>
+static int dispatch_model(mr_handle* h, int B, const mr_inputs* in, mr_outputs* out, hipStream_t st) {
+  switch (h->cfg.model) {
+    case MR_MODEL_KINEMATIC: return launch<T, MODEL_KIN>(h, B, in, out, st);
+    case MR_MODEL_DYNAMIC: return launch<T, MODEL_DYN>(h, B, in, out, st);
+    case MR_MODEL_BLENDED: return launch<T, MODEL_BLEND>(h, B, in, out, st);
+    case MR_MODEL_BLENDED_PACEJKA: return launch<T, MODEL_BLEND_PACEJKA>(h, B, in, out, st);
+    case MR_MODEL_DYNAMIC_PACEJKA: return launch<T, MODEL_DYN_PACEJKA>(h, B, in, out, st);
+  }
+  return fail(MR_ERR_ARG, "unknown model");
+}
+
+extern "C" {
+
+int mr_version(void) { return 100; }
+
+const char* mr_last_error(void) { return g_err.c_str(); }
+
+int mr_config_default(mr_config* cfg) {
+  if (!cfg) return fail(MR_ERR_ARG, "null config");
+  fill_default_config(cfg);
+  return MR_OK;
+}
+
+int mr_create(mr_handle** out, const mr_config* cfg) {
+  if (!out || !cfg) return fail(MR_ERR_ARG, "null argument");
+  if (cfg->N < 1 || cfg->N > 1000) return fail(MR_ERR_ARG, "N out of range");
+  if (cfg->model < 0 || cfg->model > 4) return fail(MR_ERR_ARG, "unknown model");
+  if (cfg->precision != MR_PREC_FP64 && cfg->precision != MR_PREC_FP32) return fail(MR_ERR_ARG, "bad precision");
+  if (cfg->max_batch < 1) return fail(MR_ERR_ARG, "max_batch < 1");
+  if (!(cfg->Ts > 0)) return fail(MR_ERR_ARG, "Ts must be > 0");
+  HIP_TRY(hipSetDevice(cfg->device));
+  mr_handle* h = new mr_handle();
+  h->cfg = *cfg;
+  h->have_tyres = 0;
+  memset(&h->tf, 0, sizeof(h->tf));
+  memset(&h->tr, 0, sizeof(h->tr));
+  h->ws_stride = cfg->max_batch;
+  h->ws_bytes = ws_bytes_per_instance(*cfg) * (size_t)cfg->max_batch;
+  hipError_t e = hipMalloc(&h->ws, h->ws_bytes);
+  if (e != hipSuccess) {
+    delete h;
+    return fail(MR_ERR_HIP, std::string("workspace hipMalloc: ") + hipGetErrorString(e));
+  }
+  *out = h;
+  return MR_OK;
+}
+
+int mr_destroy(mr_handle* h) {
+  if (!h) return MR_OK;
+  if (h->ws) (void)hipFree(h->ws);
+  delete h;
+  return MR_OK;
+}
+
+int mr_set_tyres(mr_handle* h, const double* a_front, double Fz_front, const double* a_back, double Fz_back) {
+  if (!h || !a_front || !a_back) return fail(MR_ERR_ARG, "null argument");
+  h->tf = pacejka_coef(a_front, Fz_front);
+  h->tr = pacejka_coef(a_back, Fz_back);
+  h->have_tyres = 1;
+  return MR_OK;
+}
+
+int64_t mr_workspace_bytes_per_instance(const mr_handle* h) {
+  return h ? (int64_t)ws_bytes_per_instance(h->cfg) : -1;
+}
+
+int mr_solve_batch(mr_handle* h, int32_t B, const mr_inputs* in, mr_outputs* out, void* hip_stream) {
+  if (!h || !in || !out) return fail(MR_ERR_ARG, "null argument");
+  if (B < 0 || B > h->cfg.max_batch) return fail(MR_ERR_ARG, "B exceeds max_batch");
+  if (B == 0) return MR_OK;
+  if (!in->state0 || !in->s0 || !in->cx || !in->cy || !in->max_error || !in->runtime)
+    return fail(MR_ERR_ARG, "missing input array");
+  if (!out->X || !out->U || !out->S || !out->eC || !out->eL || !out->status || !out->iters)
+    return fail(MR_ERR_ARG, "missing output array");
+  const int m = h->cfg.model;
+  if ((m == MR_MODEL_BLENDED_PACEJKA || m == MR_MODEL_DYNAMIC_PACEJKA) && !h->have_tyres)
+    return fail(MR_ERR_STATE, "Pacejka model needs mr_set_tyres");
+  HIP_TRY(hipSetDevice(h->cfg.device));
+  hipStream_t st = (hipStream_t)hip_stream;
+  if (h->cfg.precision == MR_PREC_FP64) return dispatch_model<double>(h, B, in, out, st);
+  return dispatch_model<float>(h, B, in, out, st);
+}
+
+}  // extern "C"

@@ -1,0 +1,88 @@
+// Host (g++) build of the solver core -- TEST HARNESS ONLY.
+//
+// libmpcracing_host.so runs the very same per-instance solver source as the
+// gfx950 kernels, on CPU threads, so that the solver logic can be checked
+// against the oracle in the CPU test suite (no GPU in the build container).
+// The product path (mpc-racing_amd/control/MPC.py, mpcracing.batch) never
+// loads this library; it requires libmpcracing.so and a GPU.
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+#include "mr_batch.h"
+
+using namespace mr;
+
+template <typename T, int MODEL>
+static void run(const mr_config& c, const TyreCoef<double>& tf, const TyreCoef<double>& tr, int B,
+                const mr_inputs& in, const mr_outputs& out, int nthreads) {
+  ProbParams<T> P;
+  fill_params<T>(c, tf, tr, P);
+  std::vector<T> ws((size_t)WF::NF * (c.N + 1) * (size_t)B);
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
+  for (int i = 0; i < B; ++i) {
+    WS<T> W{ws.data() + i, (int64_t)B};
+    solve_instance<T, MODEL>(P, in, out, B, i, W);
+  }
+}
+
+extern "C" {
+
+int mrh_config_default(mr_config* c) {
+  fill_default_config(c);
+  return 0;
+}
+
+int mrh_solve_batch(const mr_config* c, const double* a_front, double Fz_front, const double* a_back,
+                    double Fz_back, int B, const mr_inputs* in, mr_outputs* out, int nthreads) {
+  TyreCoef<double> tf{}, tr{};
+  if (a_front) tf = pacejka_coef(a_front, Fz_front);
+  if (a_back) tr = pacejka_coef(a_back, Fz_back);
+#define MR_CASE(T, M) run<T, M>(*c, tf, tr, B, *in, *out, nthreads)
+#define MR_MODELS(T)                                                       \
+  switch (c->model) {                                                      \
+    case MR_MODEL_KINEMATIC: MR_CASE(T, MODEL_KIN); break;                 \
+    case MR_MODEL_DYNAMIC: MR_CASE(T, MODEL_DYN); break;                   \
+    case MR_MODEL_BLENDED: MR_CASE(T, MODEL_BLEND); break;                 \
+    case MR_MODEL_BLENDED_PACEJKA: MR_CASE(T, MODEL_BLEND_PACEJKA); break; \
+    case MR_MODEL_DYNAMIC_PACEJKA: MR_CASE(T, MODEL_DYN_PACEJKA); break;   \
+    default: return -1;                                                    \
+  }
+  if (c->precision == MR_PREC_FP64) { MR_MODELS(double) } else { MR_MODELS(float) }
+  return 0;
+}
+
+// Generated dynamics (value, Jacobian, nu-weighted Hessian) at one point, fp64.
+int mrh_eval_dynamics(const mr_config* c, const double* a_front, double Fz_front, const double* a_back,
+                      double Fz_back, const double* x, const double* u, const double* nu, double* f, double* J,
+                      double* H) {
+  TyreCoef<double> tf{}, tr{};
+  if (a_front) tf = pacejka_coef(a_front, Fz_front);
+  if (a_back) tr = pacejka_coef(a_back, Fz_back);
+  ProbParams<double> P;
+  fill_params<double>(*c, tf, tr, P);
+  switch (c->model) {
+    case MR_MODEL_KINEMATIC: Dyn<double, MODEL_KIN>::fjh(P, x, u, nu, f, J, H); break;
+    case MR_MODEL_DYNAMIC: Dyn<double, MODEL_DYN>::fjh(P, x, u, nu, f, J, H); break;
+    case MR_MODEL_BLENDED: Dyn<double, MODEL_BLEND>::fjh(P, x, u, nu, f, J, H); break;
+    case MR_MODEL_BLENDED_PACEJKA: Dyn<double, MODEL_BLEND_PACEJKA>::fjh(P, x, u, nu, f, J, H); break;
+    case MR_MODEL_DYNAMIC_PACEJKA: Dyn<double, MODEL_DYN_PACEJKA>::fjh(P, x, u, nu, f, J, H); break;
+    default: return -1;
+  }
+  return 0;
+}
+
+// Pacejka jet (value, d/dalpha, d2/dalpha2) in fp64 and fp32.
+int mrh_pacejka(const double* a, double Fz, double alpha, int fp32, double* out3) {
+  TyreCoef<double> c = pacejka_coef(a, Fz);
+  if (fp32) {
+    TyreCoef<float> cf{(float)c.B, (float)c.C, (float)c.E, (float)c.BCD, (float)c.K2};
+    TyreJet<float> j = pacejka_jet(cf, (float)alpha);
+    out3[0] = j.v; out3[1] = j.d; out3[2] = j.dd;
+  } else {
+    TyreJet<double> j = pacejka_jet(c, alpha);
+    out3[0] = j.v; out3[1] = j.d; out3[2] = j.dd;
+  }
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,1081 @@
+// Per-instance primal-dual interior-point solver of the racing-MPC NLP.
+//
+// Replaces the CasADi Opti + IPOPT solve of control/MPC.py:30-181 (one
+// instance per call) by one thread per instance running the whole solve.
+//
+// Formulation (equivalent reformulation of MPC.py's NLP):
+//   stage state  x_k = [X, Y, psi, vx, vy, r, S, p_thr, p_steer, w_thr, w_steer]   (NX = 11)
+//   stage input  u_k = [thr, steer, dS]                                              (NU = 3)
+//   x_{k+1} = F(x_k, u_k):  vehicle block by the generated model (MPC.py:186-260),
+//     S+ = S + dS (S_hat differences, MPC.py:134), p+ = (thr, steer) (previous control,
+//     for the rate rows MPC.py:142-143 and the beta_delta term MPC.py:97),
+//     w+ = (k == 0 ? (thr, steer) : w) (frozen U[:,0] for the wrap-around row at i = 0,
+//     which reads U[:, -1] = U[:, N-1], MPC.py:142-143).
+//   x_0 fixed: X_0 = state0, S_0 = s0 (MPC.py:101-107), p_0 = (throttle0, steer0) so the
+//   stage-0 rate rows are the state0 rows of MPC.py:145-149.
+//   Positions and progress are kept relative to (state0.x, state0.y, s0); the global-s
+//   centerline polynomials (util.make_poly, highest order first) are Taylor-shifted to
+//   sigma = s - s0 in fp64 before the solve (same polynomial, no cancellation).
+//
+// Newton steps are computed by a Riccati recursion on the stage-wise KKT system
+// (inequalities condensed by the barrier); the algorithmic rules follow IPOPT's
+// default configuration used by MPC.py:151-161 (gradient-based objective scaling,
+// monotone barrier update, fraction to the boundary, inertia correction, filter
+// line search) plus a second-order correction that re-rolls the shooting states.
+#pragma once
+#include "mr_common.h"
+#include "gen_dynamics.h"
+
+namespace mr {
+
+enum ModelId { MODEL_KIN = 0, MODEL_DYN = 1, MODEL_BLEND = 2, MODEL_BLEND_PACEJKA = 3, MODEL_DYN_PACEJKA = 4 };
+
+constexpr int NX = 11, NU = 3, NZ = 14, NROW = 7, NI = 17;
+constexpr int NZS = NZ + 1;  // stored stage vector: z plus the elastic lane variable t (index 14)
+constexpr int JL = 14;       // slots 14, 15, 16: lane rows e_C + m + t >= 0, m - e_C + t >= 0, t >= 0
+constexpr int NH = NZ * (NZ + 1) / 2;  // packed upper triangle of the 14x14 stage Hessian
+constexpr int NP = NX * (NX + 1) / 2;  // packed P
+
+// Workspace fields per stage (SoA: element (k, f) of instance i at base[(k*NF + f)*stride + i]).
+struct WF {
+  enum {
+    Z0 = 0, Z1 = Z0 + NZS, DZ = Z1 + NZS, S0 = DZ + NZS, S1 = S0 + NI, LAM = S1 + NI, DLAM = LAM + NI,
+    DS = DLAM + NI, NUv = DS + NI, DNU = NUv + NX, H = DNU + NX, G0 = H + NH, G1 = G0 + NZ, GL = G1 + NZ,
+    J = GL + NZ, C = J + 48, P = C + NX, PV0 = P + NP, PV1 = PV0 + NX, K = PV1 + NX, K0 = K + NU * NX,
+    K1 = K0 + NU, NF = K1 + NU
+  };
+};
+
+MR_HD int hidx(int i, int j) {  // packed upper index of symmetric NZ x NZ
+  if (i > j) { int t = i; i = j; j = t; }
+  return i * NZ - (i * (i - 1)) / 2 + (j - i);
+}
+MR_HD int pidx(int i, int j) {  // packed upper index of symmetric NX x NX
+  if (i > j) { int t = i; i = j; j = t; }
+  return i * NX - (i * (i - 1)) / 2 + (j - i);
+}
+
+template <typename T>
+struct ProbParams {
+  int N, model, lane;
+  T Ts, lane_pen;  // elastic lane rows: exact-penalty weight (unscaled cost per metre)
+  // control/ControllerParameters.py FixedControllerParameters
+  T lambda_s, alpha_L, min_steer, max_steer, min_thr, max_dsteer, min_dsteer, max_dthr, min_dthr, q_vmax, v_max,
+      min_ds;
+  VehParams<T> veh;
+  TyreCoef<T> tf, tr;
+  // solver options
+  T tol, acc_tol;
+  int acc_iter, max_iter;
+};
+
+// Per-instance inputs in solver coordinates.
+template <typename T>
+struct Inst {
+  T x0[6];
+  T thr0, steer0;
+  int has_thr0, has_steer0;
+  T ax[5], ay[5];  // ascending coefficients in sigma = s - s0, minus the (X0, Y0) origin
+  T max_err, alpha_c, d_max, q_vy, beta;
+  int n;
+};
+
+template <typename T>
+struct WS {
+  T* base;
+  int64_t stride;
+  MR_HD T& operator()(int k, int f) const { return base[((int64_t)k * WF::NF + f) * stride]; }
+};
+
+// ----------------------------------------------------------------------------------------
+// Model dispatch
+// ----------------------------------------------------------------------------------------
+template <typename T, int MODEL>
+struct Dyn {
+  static MR_HD void slip(const ProbParams<T>& P, const T* x, const T* u, T& af, T& ar) {
+    const VehParams<T>& V = P.veh;
+    T vel = mr_sqrt(x[3] * x[3] + x[4] * x[4]) * T(3.6);
+    T gain = T(-0.001971664699) * vel + T(0.986547);
+    T delta = (u[1] * gain * V.max_steer / T(360)) * T(2) * T(3.14);
+    af = delta - mr_atan2(x[4] + V.lf * x[5], x[3] + T(0.1));
+    ar = -mr_atan2(x[4] - V.lr * x[5], x[3] + T(0.1));
+  }
+  // blend region: 0 -> kinematic (lambda = 0), 1 -> dynamic (lambda = 1), 2 -> blend law
+  static MR_HD int region(const ProbParams<T>& P, const T* x) {
+    T vel = mr_sqrt(x[3] * x[3] + x[4] * x[4]);
+    if (vel <= P.veh.Vblendmin) return 0;
+    if (vel >= P.veh.Vblendmax) return 1;
+    return 2;
+  }
+  static MR_HD void f(const ProbParams<T>& P, const T* x, const T* u, T* out) {
+    const VehParams<T>& V = P.veh;
+    if (MODEL == MODEL_KIN) { kin_f(V, P.Ts, x, u, out); return; }
+    if (MODEL == MODEL_DYN) { dyn_lin_f(V, P.Ts, x, u, out); return; }
+    TyreJet<T> jf{}, jr{};
+    if (MODEL == MODEL_BLEND_PACEJKA || MODEL == MODEL_DYN_PACEJKA) {
+      T af, ar;
+      slip(P, x, u, af, ar);
+      jf = pacejka_jet(P.tf, af);
+      jr = pacejka_jet(P.tr, ar);
+    }
+    if (MODEL == MODEL_DYN_PACEJKA) { dyn_tyre_f(V, P.Ts, x, u, jf, jr, out); return; }
+    int rg = region(P, x);
+    if (rg == 0) { kin_f(V, P.Ts, x, u, out); return; }
+    if (MODEL == MODEL_BLEND) {
+      if (rg == 1) dyn_lin_f(V, P.Ts, x, u, out); else blend_lin_f(V, P.Ts, x, u, out);
+    } else {
+      if (rg == 1) dyn_tyre_f(V, P.Ts, x, u, jf, jr, out); else blend_tyre_f(V, P.Ts, x, u, jf, jr, out);
+    }
+  }
+  static MR_HD void fjh(const ProbParams<T>& P, const T* x, const T* u, const T* nu, T* out, T* J, T* H) {
+    const VehParams<T>& V = P.veh;
+    if (MODEL == MODEL_KIN) { kin_fjh(V, P.Ts, x, u, nu, out, J, H); return; }
+    if (MODEL == MODEL_DYN) { dyn_lin_fjh(V, P.Ts, x, u, nu, out, J, H); return; }
+    TyreJet<T> jf{}, jr{};
+    if (MODEL == MODEL_BLEND_PACEJKA || MODEL == MODEL_DYN_PACEJKA) {
+      T af, ar;
+      slip(P, x, u, af, ar);
+      jf = pacejka_jet(P.tf, af);
+      jr = pacejka_jet(P.tr, ar);
+    }
+    if (MODEL == MODEL_DYN_PACEJKA) { dyn_tyre_fjh(V, P.Ts, x, u, nu, jf, jr, out, J, H); return; }
+    int rg = region(P, x);
+    if (rg == 0) { kin_fjh(V, P.Ts, x, u, nu, out, J, H); return; }
+    if (MODEL == MODEL_BLEND) {
+      if (rg == 1) dyn_lin_fjh(V, P.Ts, x, u, nu, out, J, H); else blend_lin_fjh(V, P.Ts, x, u, nu, out, J, H);
+    } else {
+      if (rg == 1) dyn_tyre_fjh(V, P.Ts, x, u, nu, jf, jr, out, J, H);
+      else blend_tyre_fjh(V, P.Ts, x, u, nu, jf, jr, out, J, H);
+    }
+  }
+};
+
+// ----------------------------------------------------------------------------------------
+// Centerline polynomial (util.make_poly) and the contouring / lag errors (MPC.py:71-81)
+// ----------------------------------------------------------------------------------------
+template <typename T>
+struct Err {
+  T eC, eL;
+  T gC[3], gL[3];  // gradients over (X, Y, S)
+  T hC[6], hL[6];  // packed 3x3 upper: (XX, XY, XS, YY, YS, SS)
+};
+
+template <typename T>
+MR_HD void poly3(const T* a, T s, T& g0, T& g1, T& g2, T& g3) {
+  g0 = (((a[4] * s + a[3]) * s + a[2]) * s + a[1]) * s + a[0];
+  g1 = ((T(4) * a[4] * s + T(3) * a[3]) * s + T(2) * a[2]) * s + a[1];
+  g2 = (T(12) * a[4] * s + T(6) * a[3]) * s + T(2) * a[2];
+  g3 = T(24) * a[4] * s + T(6) * a[3];
+}
+
+template <typename T>
+MR_HD void errors(const Inst<T>& I, T X, T Y, T S, Err<T>& e, bool second) {
+  T gx, dgx, hx, tx, gy, dgy, hy, ty;
+  poly3(I.ax, S, gx, dgx, hx, tx);
+  poly3(I.ay, S, gy, dgy, hy, ty);
+  T a = X - gx, b = Y - gy;
+  e.eC = dgy * a - dgx * b;
+  e.eL = -dgx * a - dgy * b;
+  e.gC[0] = dgy; e.gC[1] = -dgx; e.gC[2] = hy * a - hx * b;
+  e.gL[0] = -dgx; e.gL[1] = -dgy; e.gL[2] = -hx * a - hy * b + dgx * dgx + dgy * dgy;
+  if (second) {
+    e.hC[0] = T(0); e.hC[1] = T(0); e.hC[2] = hy; e.hC[3] = T(0); e.hC[4] = -hx;
+    e.hC[5] = ty * a - tx * b - hy * dgx + hx * dgy;
+    e.hL[0] = T(0); e.hL[1] = T(0); e.hL[2] = -hx; e.hL[3] = T(0); e.hL[4] = -hy;
+    e.hL[5] = -tx * a - ty * b + T(3) * (dgx * hx + dgy * hy);
+  }
+}
+
+template <typename T>
+MR_HD void ipow(T e, int n, T& v, T& d1, T& d2) {
+  // e^n, n e^(n-1), n(n-1) e^(n-2) for integer n >= 1
+  T p2 = T(1);
+  for (int i = 0; i < n - 2; ++i) p2 *= e;
+  if (n >= 2) {
+    d2 = T(n) * T(n - 1) * p2;
+    d1 = T(n) * p2 * e;
+    v = p2 * e * e;
+  } else {
+    d2 = T(0);
+    d1 = T(1);
+    v = e;
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// Inequality rows (MPC.py:134-149, optional lane row :135): lo <= c(z) <= hi
+// ----------------------------------------------------------------------------------------
+template <typename T>
+struct Row {
+  int active, n;
+  int idx[3];
+  T a[3];
+  T c, lo, hi;
+  int lane;
+};
+
+template <typename T>
+MR_HD void make_row(const ProbParams<T>& P, const Inst<T>& I, int k, int r, const T* z, const Err<T>* e, Row<T>& R) {
+  const int N = P.N;
+  R.active = 0; R.n = 0; R.lane = 0; R.c = T(0); R.lo = T(0); R.hi = T(0);
+  if (k == N) return;  // terminal stage: only the lane rows (lane_active)
+  switch (r) {
+    case 0:  // MPC.py:138-139 (upper = class attribute d_max, quirk)
+      R.active = 1; R.n = 1; R.idx[0] = 11; R.a[0] = T(1); R.c = z[11]; R.lo = P.min_thr; R.hi = I.d_max; break;
+    case 1:  // MPC.py:140-141
+      R.active = 1; R.n = 1; R.idx[0] = 12; R.a[0] = T(1); R.c = z[12]; R.lo = P.min_steer; R.hi = P.max_steer; break;
+    case 2:  // MPC.py:134: 0.1 <= S_i - S_{i-1} <= Ts*v_max
+      R.active = 1; R.n = 1; R.idx[0] = 13; R.a[0] = T(1); R.c = z[13]; R.lo = P.min_ds; R.hi = P.Ts * P.v_max; break;
+    case 3:  // MPC.py:142 (k >= 1) / :145-146 (k == 0 against state0.throttle)
+      if (k >= 1 || I.has_thr0) {
+        R.active = 1; R.n = 2; R.idx[0] = 11; R.a[0] = T(1); R.idx[1] = 7; R.a[1] = T(-1);
+        R.c = z[11] - z[7]; R.lo = P.min_dthr; R.hi = P.max_dthr;
+      }
+      break;
+    case 4:  // MPC.py:143 / :148-149
+      if (k >= 1 || I.has_steer0) {
+        R.active = 1; R.n = 2; R.idx[0] = 12; R.a[0] = T(1); R.idx[1] = 8; R.a[1] = T(-1);
+        R.c = z[12] - z[8]; R.lo = P.min_dsteer; R.hi = P.max_dsteer;
+      }
+      break;
+    case 5:  // MPC.py:142 at i = 0: U[0,0] - U[0,N-1] via the frozen copy w
+      if (k == N - 1 && N >= 2) {
+        R.active = 1; R.n = 2; R.idx[0] = 9; R.a[0] = T(1); R.idx[1] = 11; R.a[1] = T(-1);
+        R.c = z[9] - z[11]; R.lo = P.min_dthr; R.hi = P.max_dthr;
+      }
+      break;
+    case 6:  // MPC.py:143 at i = 0
+      if (k == N - 1 && N >= 2) {
+        R.active = 1; R.n = 2; R.idx[0] = 10; R.a[0] = T(1); R.idx[1] = 12; R.a[1] = T(-1);
+        R.c = z[10] - z[12]; R.lo = P.min_dsteer; R.hi = P.max_dsteer;
+      }
+      break;
+  }
+}
+
+// Lane rows on states i = 1..N (the commented MPC.py:135), elastic form:
+//   e_C + m + t >= 0,  m - e_C + t >= 0,  t >= 0, cost lane_pen * t (exact penalty: t* = 0
+//   and the same KKT point as the hard row whenever that NLP is feasible and lane_pen > |lambda*|).
+template <typename T>
+MR_HD bool lane_active(const ProbParams<T>& P, int k) { return P.lane && k >= 1; }
+
+template <typename T>
+MR_HD void lane_d(const Inst<T>& I, T eC, T t, T* d) {
+  d[0] = eC + I.max_err + t;
+  d[1] = I.max_err - eC + t;
+  d[2] = t;
+}
+
+// ----------------------------------------------------------------------------------------
+// Stage cost (MPC.py:86-98), scaled by obj_scale.  Stage 0 has no cost.
+// ----------------------------------------------------------------------------------------
+template <typename T>
+MR_HD T stage_cost(const ProbParams<T>& P, const Inst<T>& I, int k, const T* z, const Err<T>& e, T sc, T* g, T* H) {
+  // g: gradient (NZ), H: packed Hessian (NH) accumulated; either may be null
+  if (k == 0) return T(0);
+  const int N = P.N;
+  T val = T(0);
+  // q_v_y * vy^2
+  T vy = z[4];
+  val += I.q_vy * vy * vy;
+  if (g) g[4] += sc * T(2) * I.q_vy * vy;
+  if (H) H[hidx(4, 4)] += sc * T(2) * I.q_vy;
+  // exp(q_v_max (vx - v_max))
+  T ex = mr_exp(P.q_vmax * (z[3] - P.v_max));
+  val += ex;
+  if (g) g[3] += sc * P.q_vmax * ex;
+  if (H) H[hidx(3, 3)] += sc * P.q_vmax * P.q_vmax * ex;
+  // alpha_c eC^n + alpha_L eL^2 over (X, Y, S) = indices (0, 1, 6)
+  T cv, c1, c2;
+  ipow(e.eC, I.n, cv, c1, c2);
+  val += I.alpha_c * cv + P.alpha_L * e.eL * e.eL;
+  const int id3[3] = {0, 1, 6};
+  if (g) {
+    for (int a = 0; a < 3; ++a)
+      g[id3[a]] += sc * (I.alpha_c * c1 * e.gC[a] + T(2) * P.alpha_L * e.eL * e.gL[a]);
+  }
+  if (H) {
+    int q = 0;
+    for (int a = 0; a < 3; ++a)
+      for (int b = a; b < 3; ++b, ++q) {
+        T hv = I.alpha_c * (c2 * e.gC[a] * e.gC[b] + c1 * e.hC[q]) +
+               T(2) * P.alpha_L * (e.gL[a] * e.gL[b] + e.eL * e.hL[q]);
+        H[hidx(id3[a], id3[b])] += sc * hv;
+      }
+  }
+  if (k == N) {
+    // terminal: -lambda_s * S_N (MPC.py:86)
+    val += -P.lambda_s * z[6];
+    if (g) g[6] += -sc * P.lambda_s;
+  } else {
+    // beta_delta (U1_i - U1_{i-1})^2 with U1_{i-1} = p_steer (MPC.py:97)
+    T du = z[12] - z[8];
+    val += I.beta * du * du;
+    if (g) { g[12] += sc * T(2) * I.beta * du; g[8] -= sc * T(2) * I.beta * du; }
+    if (H) {
+      H[hidx(12, 12)] += sc * T(2) * I.beta;
+      H[hidx(8, 8)] += sc * T(2) * I.beta;
+      H[hidx(8, 12)] -= sc * T(2) * I.beta;
+    }
+  }
+  return sc * val;
+}
+
+// Augmented dynamics value (vehicle block + linear S, p, w parts).
+template <typename T, int MODEL>
+MR_HD void faug(const ProbParams<T>& P, int k, const T* z, T* xn) {
+  Dyn<T, MODEL>::f(P, z, z + NX, xn);
+  xn[6] = z[6] + z[13];
+  xn[7] = z[11];
+  xn[8] = z[12];
+  xn[9] = (k == 0) ? z[11] : z[9];
+  xn[10] = (k == 0) ? z[12] : z[10];
+}
+
+// ----------------------------------------------------------------------------------------
+// Small dense helpers
+// ----------------------------------------------------------------------------------------
+template <typename T>
+MR_HD bool chol3(T* R, T* L) {  // R packed upper 3x3 (00,01,02,11,12,22) -> L lower (00,10,11,20,21,22)
+  T l00 = R[0];
+  if (!(l00 > T(0))) return false;
+  l00 = mr_sqrt(l00);
+  T l10 = R[1] / l00, l20 = R[2] / l00;
+  T d1 = R[3] - l10 * l10;
+  if (!(d1 > T(0))) return false;
+  T l11 = mr_sqrt(d1);
+  T l21 = (R[4] - l20 * l10) / l11;
+  T d2 = R[5] - l20 * l20 - l21 * l21;
+  if (!(d2 > T(0))) return false;
+  T l22 = mr_sqrt(d2);
+  L[0] = l00; L[1] = l10; L[2] = l11; L[3] = l20; L[4] = l21; L[5] = l22;
+  return true;
+}
+template <typename T>
+MR_HD void chol3_solve(const T* L, T* b) {  // solves (L L^T) x = b in place
+  T y0 = b[0] / L[0];
+  T y1 = (b[1] - L[1] * y0) / L[2];
+  T y2 = (b[2] - L[3] * y0 - L[4] * y1) / L[5];
+  T x2 = y2 / L[5];
+  T x1 = (y1 - L[4] * x2) / L[2];
+  T x0 = (y0 - L[1] * x1 - L[3] * x2) / L[0];
+  b[0] = x0; b[1] = x1; b[2] = x2;
+}
+
+// y = A v for the augmented dynamics Jacobian w.r.t. x (11x11); J is the 6x8 vehicle Jacobian
+template <typename T>
+MR_HD void apply_A(const T* J, int k, const T* v, T* y) {
+  for (int i = 0; i < 6; ++i) {
+    T acc = T(0);
+    for (int j = 0; j < 6; ++j) acc += J[i * 8 + j] * v[j];
+    y[i] = acc;
+  }
+  y[6] = v[6];
+  y[7] = T(0);
+  y[8] = T(0);
+  y[9] = (k == 0) ? T(0) : v[9];
+  y[10] = (k == 0) ? T(0) : v[10];
+}
+// y = B w (11x3)
+template <typename T>
+MR_HD void apply_B(const T* J, int k, const T* w, T* y) {
+  for (int i = 0; i < 6; ++i) y[i] = J[i * 8 + 6] * w[0] + J[i * 8 + 7] * w[1];
+  y[6] = w[2];
+  y[7] = w[0];
+  y[8] = w[1];
+  y[9] = (k == 0) ? w[0] : T(0);
+  y[10] = (k == 0) ? w[1] : T(0);
+}
+// y = A^T v (11)
+template <typename T>
+MR_HD void apply_At(const T* J, int k, const T* v, T* y) {
+  for (int j = 0; j < 6; ++j) {
+    T acc = T(0);
+    for (int i = 0; i < 6; ++i) acc += J[i * 8 + j] * v[i];
+    y[j] = acc;
+  }
+  y[6] = v[6];
+  y[7] = T(0);
+  y[8] = T(0);
+  y[9] = (k == 0) ? T(0) : v[9];
+  y[10] = (k == 0) ? T(0) : v[10];
+}
+// y = B^T v (3)
+template <typename T>
+MR_HD void apply_Bt(const T* J, int k, const T* v, T* y) {
+  T a0 = v[7], a1 = v[8];
+  if (k == 0) { a0 += v[9]; a1 += v[10]; }
+  for (int i = 0; i < 6; ++i) { a0 += J[i * 8 + 6] * v[i]; a1 += J[i * 8 + 7] * v[i]; }
+  y[0] = a0; y[1] = a1; y[2] = v[6];
+}
+
+// ----------------------------------------------------------------------------------------
+// The solver
+// ----------------------------------------------------------------------------------------
+struct SolveOut {
+  int status, iters;
+  double kkt, obj;
+};
+
+constexpr int FMAX = 16;
+
+template <typename T, int MODEL>
+struct Solver {
+  const ProbParams<T>& P;
+  const Inst<T>& I;
+  WS<T> W;
+  int N;
+  // iteration state
+  int cur;          // which z/s buffer holds the current iterate
+  T mu, sc, delta_last;
+  T alpha_p, alpha_d;  // last accepted primal / dual step (lazy update)
+  T theta_max, theta_min;
+  T filt_th[FMAX], filt_ph[FMAX];
+  int nfilt;
+  // iteration aggregates (eval sweep)
+  T stat_max, pr_max, theta, slam_max, slam_min, nu1, lam1, fval, logs;
+  int me, mi;
+
+  MR_HD Solver(const ProbParams<T>& P_, const Inst<T>& I_, WS<T> W_) : P(P_), I(I_), W(W_), N(P_.N) {}
+
+  MR_HD int zf(int b) const { return b ? WF::Z1 : WF::Z0; }
+  MR_HD int sf(int b) const { return b ? WF::S1 : WF::S0; }
+
+  MR_HD void load_z(int k, int b, T* z) const {  // z[NZS]
+    const int f = zf(b);
+    for (int i = 0; i < NZS; ++i) z[i] = W(k, f + i);
+    if (k == N) { z[11] = T(0); z[12] = T(0); z[13] = T(0); }
+  }
+  MR_HD void store_z(int k, int b, const T* z) const {
+    const int f = zf(b);
+    for (int i = 0; i < NZS; ++i) W(k, f + i) = z[i];
+  }
+
+  // one-sided row values d_j (slots 0..16) of stage k at z; returns row-active mask bits
+  MR_HD void row_values(int k, const T* z, const Err<T>& e, T* d, int* act, Row<T>* rows) const {
+    for (int r = 0; r < NROW; ++r) {
+      make_row(P, I, k, r, z, &e, rows[r]);
+      act[2 * r] = act[2 * r + 1] = rows[r].active;
+      d[2 * r] = rows[r].c - rows[r].lo;
+      d[2 * r + 1] = rows[r].hi - rows[r].c;
+    }
+    const int la = lane_active(P, k) ? 1 : 0;
+    act[JL] = act[JL + 1] = act[JL + 2] = la;
+    lane_d(I, e.eC, z[14], d + JL);
+  }
+
+  // ---------------- initialisation (MPC.py:100-131) ----------------
+  // u_init: optional strided [2][N] initial controls of this instance (element (r, k) at u_init[(r*N+k)*ustride])
+  MR_HD void init(const double* u_init, int64_t ustride) {
+    cur = 0;
+    T z[NZS], zn[NX];
+    for (int i = 0; i < NZS; ++i) z[i] = T(0);
+    for (int i = 0; i < 6; ++i) z[i] = I.x0[i];
+    z[7] = I.has_thr0 ? I.thr0 : T(0);
+    z[8] = I.has_steer0 ? I.steer0 : T(0);
+    T gmax = T(0);
+    for (int k = 0; k <= N; ++k) {
+      if (k < N) {
+        if (u_init) { z[11] = T(u_init[(int64_t)k * ustride]); z[12] = T(u_init[(int64_t)(N + k) * ustride]); }
+        else { z[11] = I.thr0; z[12] = I.steer0; }
+        z[13] = P.Ts * P.v_max;  // S_i = s0 + i*Ts*v_max (MPC.py:127)
+      } else {
+        z[11] = z[12] = z[13] = T(0);
+      }
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      z[14] = lane_active(P, k) ? mr_max(mr_abs(e.eC) - I.max_err, T(0)) + T(1e-2) : T(0);
+      store_z(k, 0, z);
+      // objective gradient for the gradient-based scaling (elastic variables excluded)
+      T g[NZ];
+      for (int i = 0; i < NZ; ++i) g[i] = T(0);
+      stage_cost(P, I, k, z, e, T(1), g, (T*)nullptr);
+      for (int i = 0; i < NZ; ++i) gmax = mr_max(gmax, mr_abs(g[i]));
+      if (k < N) {
+        faug<T, MODEL>(P, k, z, zn);
+        for (int i = 0; i < NX; ++i) z[i] = zn[i];
+      }
+    }
+    sc = gmax > T(0) ? mr_min(T(1), T(100) / gmax) : T(1);
+    // slacks (IPOPT bound push), multipliers
+    T th = T(0);
+    for (int k = 0; k <= N; ++k) {
+      load_z(k, 0, z);
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      T d[NI];
+      int act[NI];
+      Row<T> rows[NROW];
+      row_values(k, z, e, d, act, rows);
+      for (int j = 0; j < NI; ++j) {
+        T push;
+        if (j < JL) {
+          const Row<T>& R = rows[j / 2];
+          T bnd = (j & 1) ? mr_abs(R.hi) : mr_abs(R.lo);
+          push = mr_min(T(1e-2) * mr_max(T(1), bnd), T(1e-2) * (R.hi - R.lo));
+        } else {
+          push = j < JL + 2 ? T(1e-2) * mr_max(T(1), I.max_err) : T(1e-2);
+        }
+        T s = act[j] ? mr_max(d[j], push) : T(1);
+        W(k, WF::S0 + j) = s;
+        W(k, WF::LAM + j) = act[j] ? T(1) : T(0);
+        W(k, WF::DLAM + j) = T(0);
+        if (act[j]) th += mr_abs(d[j] - s);
+      }
+      for (int i = 0; i < NX; ++i) { W(k, WF::NUv + i) = T(0); W(k, WF::DNU + i) = T(0); }
+    }
+    mu = T(0.1);
+    delta_last = T(0);
+    alpha_p = alpha_d = T(0);
+    theta_max = T(1e4) * mr_max(T(1), th);
+    theta_min = T(1e-4) * mr_max(T(1), th);
+    nfilt = 0;
+  }
+
+  // Elastic lane variable: condensed 1x1 block of the stage Newton system.
+  //   h_tt = sum sig_j, h_tz = (sig_0 - sig_1) grad(eC), g_t = sc*pen + sum_j (sig_j r_j - mu/s_j)
+  MR_HD void lane_block(int k, int b, const T* d, T& htt, T& hd, T& gt0, T& gt1) const {
+    htt = T(0); gt0 = sc * P.lane_pen; gt1 = T(0);
+    T sig[3];
+    for (int q = 0; q < 3; ++q) {
+      T s = W(k, sf(b) + JL + q), lam = W(k, WF::LAM + JL + q);
+      sig[q] = lam / s;
+      htt += sig[q];
+      gt0 += sig[q] * (d[JL + q] - s);
+      gt1 -= T(1) / s;
+    }
+    hd = sig[0] - sig[1];  // h_tz = hd * grad(eC)
+  }
+
+  // ---------------- sweep 1: evaluation, KKT error, stage QP data ----------------
+  // Applies the lazy dual update of the previous accepted step first.
+  MR_HD void eval_sweep(T mu_prev) {
+    const T kappa_sigma = T(1e10);
+    stat_max = pr_max = theta = T(0);
+    slam_max = T(0);
+    slam_min = T(1e30);
+    nu1 = lam1 = fval = logs = T(0);
+    me = NX * (N + 1);
+    mi = 0;
+    T z[NZS], znext[NZS], nuk[NX], nun[NX];
+    load_z(0, cur, z);
+    for (int i = 0; i < NX; ++i) nuk[i] = T(0);
+    for (int k = 0; k <= N; ++k) {
+      // multipliers of x_{k+1} = F(x_k, u_k): lazy update nu += alpha_p * dnu
+      if (k < N) {
+        for (int i = 0; i < NX; ++i) {
+          T v = W(k + 1, WF::NUv + i) + alpha_p * W(k + 1, WF::DNU + i);
+          W(k + 1, WF::NUv + i) = v;
+          nun[i] = v;
+          nu1 += mr_abs(v);
+        }
+        load_z(k + 1, cur, znext);
+      }
+      T H[NH], g0[NZ], g1[NZ], gl[NZ], st[NZ];
+      for (int i = 0; i < NH; ++i) H[i] = T(0);
+      for (int i = 0; i < NZ; ++i) { g0[i] = g1[i] = gl[i] = st[i] = T(0); }
+      if (k < N) {
+        T Hd[36], J[48], fx[6];
+        Dyn<T, MODEL>::fjh(P, z, z + NX, nun, fx, J, Hd);
+        // vehicle-block Hessian over (x0..x5, u0, u1) -> stage indices
+        const int map[8] = {0, 1, 2, 3, 4, 5, 11, 12};
+        int q = 0;
+        for (int a = 0; a < 8; ++a)
+          for (int bb = a; bb < 8; ++bb, ++q) H[hidx(map[a], map[bb])] += Hd[q];
+        // defect c_k = F(x_k, u_k) - x_{k+1}
+        T c[NX];
+        for (int i = 0; i < 6; ++i) c[i] = fx[i] - znext[i];
+        c[6] = z[6] + z[13] - znext[6];
+        c[7] = z[11] - znext[7];
+        c[8] = z[12] - znext[8];
+        c[9] = (k == 0 ? z[11] : z[9]) - znext[9];
+        c[10] = (k == 0 ? z[12] : z[10]) - znext[10];
+        for (int i = 0; i < NX; ++i) {
+          W(k, WF::C + i) = c[i];
+          pr_max = mr_max(pr_max, mr_abs(c[i]));
+          theta += mr_abs(c[i]);
+        }
+        for (int i = 0; i < 48; ++i) W(k, WF::J + i) = J[i];
+        // A^T nu_{k+1}, B^T nu_{k+1} into the stationarity residual
+        T at[NX], bt[NU];
+        apply_At(J, k, nun, at);
+        apply_Bt(J, k, nun, bt);
+        for (int i = 0; i < NX; ++i) st[i] += at[i];
+        for (int i = 0; i < NU; ++i) st[NX + i] += bt[i];
+      }
+      // cost
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, true);
+      fval += stage_cost(P, I, k, z, e, sc, gl, H);
+      for (int i = 0; i < NZ; ++i) { g0[i] += gl[i]; st[i] += gl[i]; }
+      // -nu_k on the state part (k >= 1)
+      if (k >= 1) for (int i = 0; i < NX; ++i) st[i] -= nuk[i];
+      // inequality rows: lazy dual update, barrier terms
+      T d[NI];
+      int act[NI];
+      Row<T> rows[NROW];
+      row_values(k, z, e, d, act, rows);
+      T lam_j[NI], s_j[NI];
+      for (int j = 0; j < NI; ++j) {
+        if (!act[j]) continue;
+        T s = W(k, sf(cur) + j);
+        T lam = W(k, WF::LAM + j) + alpha_d * W(k, WF::DLAM + j);
+        lam = mr_min(mr_max(lam, mu_prev / (kappa_sigma * s)), kappa_sigma * mu_prev / s);
+        W(k, WF::LAM + j) = lam;
+        lam_j[j] = lam;
+        s_j[j] = s;
+        T rd = d[j] - s;
+        pr_max = mr_max(pr_max, mr_abs(rd));
+        theta += mr_abs(rd);
+        T sl = s * lam;
+        slam_max = mr_max(slam_max, sl);
+        slam_min = mr_min(slam_min, sl);
+        lam1 += mr_abs(lam);
+        logs += mr_log(s);
+        mi += 1;
+      }
+      for (int r = 0; r < NROW; ++r) {
+        const Row<T>& R = rows[r];
+        if (!R.active) continue;
+        T sig_sum = T(0), gsc0 = T(0), gsc1 = T(0), lamdiff = T(0);
+        for (int sd = 0; sd < 2; ++sd) {
+          int j = 2 * r + sd;
+          T sig = lam_j[j] / s_j[j];
+          T sgn = sd == 0 ? T(1) : T(-1);
+          sig_sum += sig;
+          gsc0 += sgn * sig * (d[j] - s_j[j]);
+          gsc1 += -sgn / s_j[j];
+          lamdiff += sgn * lam_j[j];
+        }
+        for (int a = 0; a < R.n; ++a) {
+          g0[R.idx[a]] += R.a[a] * gsc0;
+          g1[R.idx[a]] += R.a[a] * gsc1;
+          st[R.idx[a]] -= lamdiff * R.a[a];
+          for (int bb = a; bb < R.n; ++bb) H[hidx(R.idx[a], R.idx[bb])] += sig_sum * R.a[a] * R.a[bb];
+        }
+      }
+      if (lane_active(P, k)) {
+        // rows e_C + m + t (slot JL) and m - e_C + t (JL+1) in z; t condensed out
+        const int id3[3] = {0, 1, 6};
+        T s0 = s_j[JL], s1 = s_j[JL + 1];
+        T sig0 = lam_j[JL] / s0, sig1 = lam_j[JL + 1] / s1;
+        T lamdiff = lam_j[JL] - lam_j[JL + 1];
+        T gz0 = sig0 * (d[JL] - s0) - sig1 * (d[JL + 1] - s1);
+        T gz1 = -T(1) / s0 + T(1) / s1;
+        T htt, hd, gt0, gt1;
+        lane_block(k, cur, d, htt, hd, gt0, gt1);
+        int q = 0;
+        for (int a = 0; a < 3; ++a) {
+          g0[id3[a]] += e.gC[a] * (gz0 - hd * gt0 / htt);
+          g1[id3[a]] += e.gC[a] * (gz1 - hd * gt1 / htt);
+          st[id3[a]] -= lamdiff * e.gC[a];
+          for (int bb = a; bb < 3; ++bb, ++q) {
+            H[hidx(id3[a], id3[bb])] += (sig0 + sig1 - hd * hd / htt) * e.gC[a] * e.gC[bb] - lamdiff * e.hC[q];
+          }
+        }
+        fval += sc * P.lane_pen * z[14];
+        T stt = sc * P.lane_pen - lam_j[JL] - lam_j[JL + 1] - lam_j[JL + 2];
+        stat_max = mr_max(stat_max, mr_abs(stt));
+      }
+      // stationarity: x-part for k >= 1, u-part for k < N
+      if (k >= 1) for (int i = 0; i < NX; ++i) stat_max = mr_max(stat_max, mr_abs(st[i]));
+      if (k < N) for (int i = NX; i < NZ; ++i) stat_max = mr_max(stat_max, mr_abs(st[i]));
+      for (int i = 0; i < NH; ++i) W(k, WF::H + i) = H[i];
+      for (int i = 0; i < NZ; ++i) { W(k, WF::G0 + i) = g0[i]; W(k, WF::G1 + i) = g1[i]; W(k, WF::GL + i) = gl[i]; }
+      // advance
+      if (k < N) {
+        for (int i = 0; i < NZS; ++i) z[i] = znext[i];
+        for (int i = 0; i < NX; ++i) nuk[i] = nun[i];
+      }
+    }
+  }
+
+  MR_HD T kkt_error(T m) const {
+    const T smax = T(100);
+    T sd = mr_max(smax, (nu1 + lam1) / T(me + (mi > 0 ? mi : 1))) / smax;
+    T scm = mr_max(smax, lam1 / T(mi > 0 ? mi : 1)) / smax;
+    T cerr = mr_max(mr_abs(slam_max - m), mr_abs(m - slam_min));
+    if (mi == 0) cerr = T(0);
+    return mr_max(mr_max(stat_max / sd, pr_max), cerr / scm);
+  }
+
+  // ---------------- sweep 2: Riccati factorisation (backward) ----------------
+  MR_HD bool riccati(T delta) {
+    T Pm[NP], p0[NX], p1[NX];
+    {
+      const int k = N;
+      for (int i = 0; i < NX; ++i)
+        for (int j = i; j < NX; ++j) Pm[pidx(i, j)] = W(k, WF::H + hidx(i, j)) + (i == j ? delta : T(0));
+      for (int i = 0; i < NX; ++i) { p0[i] = W(k, WF::G0 + i); p1[i] = W(k, WF::G1 + i); }
+      for (int i = 0; i < NP; ++i) W(k, WF::P + i) = Pm[i];
+      for (int i = 0; i < NX; ++i) { W(k, WF::PV0 + i) = p0[i]; W(k, WF::PV1 + i) = p1[i]; }
+    }
+    for (int k = N - 1; k >= 0; --k) {
+      T J[48], c[NX];
+      for (int i = 0; i < 48; ++i) J[i] = W(k, WF::J + i);
+      for (int i = 0; i < NX; ++i) c[i] = W(k, WF::C + i);
+      // PA (11x11) column by column and PB (11x3)
+      T PA[NX][NX], PB[NX][NU];
+      for (int j = 0; j < NX; ++j) {
+        T col[NX], e[NX];
+        for (int i = 0; i < NX; ++i) e[i] = T(0);
+        e[j] = T(1);
+        apply_A(J, k, e, col);  // column j of A
+        for (int i = 0; i < NX; ++i) {
+          T acc = T(0);
+          for (int l = 0; l < NX; ++l) acc += Pm[pidx(i, l)] * col[l];
+          PA[i][j] = acc;
+        }
+      }
+      for (int j = 0; j < NU; ++j) {
+        T col[NX], e3[NU] = {T(0), T(0), T(0)};
+        e3[j] = T(1);
+        apply_B(J, k, e3, col);
+        for (int i = 0; i < NX; ++i) {
+          T acc = T(0);
+          for (int l = 0; l < NX; ++l) acc += Pm[pidx(i, l)] * col[l];
+          PB[i][j] = acc;
+        }
+      }
+      // Rhat = R + B^T P B, Shat = S + B^T P A, Qhat = Q + A^T P A
+      T Rh[6];
+      {
+        int q = 0;
+        for (int a = 0; a < NU; ++a)
+          for (int b = a; b < NU; ++b, ++q) {
+            T colb[NX];
+            for (int i = 0; i < NX; ++i) colb[i] = PB[i][b];
+            T bt[NU];
+            apply_Bt(J, k, colb, bt);
+            Rh[q] = W(k, WF::H + hidx(NX + a, NX + b)) + bt[a] + (a == b ? delta : T(0));
+          }
+      }
+      T Sh[NU][NX];
+      for (int j = 0; j < NX; ++j) {
+        T colj[NX], bt[NU];
+        for (int i = 0; i < NX; ++i) colj[i] = PA[i][j];
+        apply_Bt(J, k, colj, bt);
+        for (int a = 0; a < NU; ++a) Sh[a][j] = W(k, WF::H + hidx(j, NX + a)) + bt[a];
+      }
+      T L[6];
+      if (!chol3(Rh, L)) return false;
+      // vector parts
+      T pc0[NX];
+      for (int i = 0; i < NX; ++i) {
+        T acc = p0[i];
+        for (int l = 0; l < NX; ++l) acc += Pm[pidx(i, l)] * c[l];
+        pc0[i] = acc;
+      }
+      T rh0[NU], rh1[NU];
+      apply_Bt(J, k, pc0, rh0);
+      apply_Bt(J, k, p1, rh1);
+      for (int a = 0; a < NU; ++a) {
+        rh0[a] += W(k, WF::G0 + NX + a);
+        rh1[a] += W(k, WF::G1 + NX + a);
+      }
+      T k0[NU] = {-rh0[0], -rh0[1], -rh0[2]}, k1[NU] = {-rh1[0], -rh1[1], -rh1[2]};
+      chol3_solve(L, k0);
+      chol3_solve(L, k1);
+      T Kg[NU][NX];
+      for (int j = 0; j < NX; ++j) {
+        T col[NU] = {-Sh[0][j], -Sh[1][j], -Sh[2][j]};
+        chol3_solve(L, col);
+        for (int a = 0; a < NU; ++a) Kg[a][j] = col[a];
+      }
+      // new P = Q + A^T P A + Sh^T K ; p = q + A^T pc + Sh^T kff
+      T Pn[NP];
+      for (int j = 0; j < NX; ++j) {
+        T colj[NX], at[NX];
+        for (int i = 0; i < NX; ++i) colj[i] = PA[i][j];
+        apply_At(J, k, colj, at);  // column j of A^T P A
+        for (int i = 0; i <= j; ++i) {
+          T v = at[i] + W(k, WF::H + hidx(i, j)) + (i == j ? delta : T(0));
+          for (int a = 0; a < NU; ++a) v += Sh[a][i] * Kg[a][j];
+          Pn[pidx(i, j)] = v;
+        }
+      }
+      T pn0[NX], pn1[NX], t0[NX], t1[NX];
+      apply_At(J, k, pc0, t0);
+      apply_At(J, k, p1, t1);
+      for (int i = 0; i < NX; ++i) {
+        T v0 = W(k, WF::G0 + i) + t0[i], v1 = W(k, WF::G1 + i) + t1[i];
+        for (int a = 0; a < NU; ++a) { v0 += Sh[a][i] * k0[a]; v1 += Sh[a][i] * k1[a]; }
+        pn0[i] = v0;
+        pn1[i] = v1;
+      }
+      for (int a = 0; a < NU; ++a) {
+        for (int j = 0; j < NX; ++j) W(k, WF::K + a * NX + j) = Kg[a][j];
+        W(k, WF::K0 + a) = k0[a];
+        W(k, WF::K1 + a) = k1[a];
+      }
+      for (int i = 0; i < NP; ++i) { Pm[i] = Pn[i]; W(k, WF::P + i) = Pn[i]; }
+      for (int i = 0; i < NX; ++i) {
+        p0[i] = pn0[i]; p1[i] = pn1[i];
+        W(k, WF::PV0 + i) = pn0[i]; W(k, WF::PV1 + i) = pn1[i];
+      }
+    }
+    return true;
+  }
+
+  // ---------------- sweep 3: forward substitution, slack/dual steps ----------------
+  // fraction-to-boundary primal/dual step and the directional derivative of phi_mu
+  MR_HD void forward(T& ap, T& ad, T& gphi) {
+    const T tau = mr_max(T(0.99), T(1) - mu);
+    ap = T(1);
+    ad = T(1);
+    gphi = T(0);
+    T dx[NX];
+    for (int i = 0; i < NX; ++i) dx[i] = T(0);
+    T z[NZS];
+    for (int k = 0; k <= N; ++k) {
+      T dz[NZS];
+      for (int i = 0; i < NX; ++i) dz[i] = dx[i];
+      if (k < N) {
+        for (int a = 0; a < NU; ++a) {
+          T v = W(k, WF::K0 + a) + mu * W(k, WF::K1 + a);
+          for (int j = 0; j < NX; ++j) v += W(k, WF::K + a * NX + j) * dx[j];
+          dz[NX + a] = v;
+        }
+      } else {
+        dz[11] = dz[12] = dz[13] = T(0);
+      }
+      for (int i = 0; i < NZ; ++i) gphi += W(k, WF::GL + i) * dz[i];
+      // rows
+      load_z(k, cur, z);
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      T d[NI];
+      int act[NI];
+      Row<T> rows[NROW];
+      row_values(k, z, e, d, act, rows);
+      T adz[NI];
+      for (int r = 0; r < NROW; ++r) {
+        T v = T(0);
+        for (int a = 0; a < rows[r].n; ++a) v += rows[r].a[a] * dz[rows[r].idx[a]];
+        adz[2 * r] = v;
+        adz[2 * r + 1] = -v;
+      }
+      dz[14] = T(0);
+      if (lane_active(P, k)) {
+        T htt, hd, gt0, gt1;
+        lane_block(k, cur, d, htt, hd, gt0, gt1);
+        T gdz = e.gC[0] * dz[0] + e.gC[1] * dz[1] + e.gC[2] * dz[6];
+        T dt = -(hd * gdz + gt0 + mu * gt1) / htt;
+        dz[14] = dt;
+        adz[JL] = gdz + dt;
+        adz[JL + 1] = -gdz + dt;
+        adz[JL + 2] = dt;
+        gphi += sc * P.lane_pen * dt;
+      }
+      for (int i = 0; i < NZS; ++i) W(k, WF::DZ + i) = dz[i];
+      for (int j = 0; j < NI; ++j) {
+        if (!act[j]) continue;
+        T s = W(k, sf(cur) + j), lam = W(k, WF::LAM + j);
+        T ds = adz[j] + (d[j] - s);
+        T dl = mu / s - lam - (lam / s) * ds;
+        W(k, WF::DS + j) = ds;
+        W(k, WF::DLAM + j) = dl;
+        gphi -= mu * ds / s;
+        if (ds < T(0)) ap = mr_min(ap, -tau * s / ds);
+        if (dl < T(0)) ad = mr_min(ad, -tau * lam / dl);
+      }
+      if (k < N) {
+        T J[48], t[NX], tb[NX];
+        for (int i = 0; i < 48; ++i) J[i] = W(k, WF::J + i);
+        apply_A(J, k, dx, t);
+        apply_B(J, k, dz + NX, tb);
+        for (int i = 0; i < NX; ++i) dx[i] = t[i] + tb[i] + W(k, WF::C + i);
+        // costate nu_{k+1} = P_{k+1} dx_{k+1} + p_{k+1}
+        for (int i = 0; i < NX; ++i) {
+          T v = W(k + 1, WF::PV0 + i) + mu * W(k + 1, WF::PV1 + i);
+          for (int l = 0; l < NX; ++l) v += W(k + 1, WF::P + pidx(i, l)) * dx[l];
+          W(k + 1, WF::DNU + i) = v - W(k + 1, WF::NUv + i);
+        }
+      }
+    }
+  }
+
+  // ---------------- sweep 4: line-search trial point ----------------
+  // Writes the trial iterate into buffer 1-cur; returns false if a slack is not positive.
+  MR_HD bool trial(T alpha, bool soc, T& th_t, T& ph_t) {
+    const int nb = 1 - cur;
+    th_t = T(0);
+    T fv = T(0), lg = T(0);
+    T z[NZS], zt[NZS], zpl[NZS], zroll[NX];
+    bool ok = true;
+    for (int k = 0; k <= N; ++k) {
+      load_z(k, cur, z);
+      for (int i = 0; i < NZS; ++i) zt[i] = z[i] + alpha * W(k, WF::DZ + i);
+      if (k == 0)
+        for (int i = 0; i < NX; ++i) zt[i] = z[i];  // x_0 fixed
+      if (k == N) { zt[11] = zt[12] = zt[13] = T(0); }
+      for (int i = 0; i < NZS; ++i) zpl[i] = zt[i];
+      if (soc && k >= 1)
+        for (int i = 0; i < NX; ++i) zt[i] = zroll[i];
+      // rows: slack trial s + alpha ds (+ SOC shift d(z_soc) - d(z_plain))
+      Err<T> e, ep;
+      errors(I, zt[0], zt[1], zt[6], e, false);
+      T d[NI], dp[NI];
+      int act[NI];
+      Row<T> rows[NROW];
+      row_values(k, zt, e, d, act, rows);
+      if (soc) {
+        errors(I, zpl[0], zpl[1], zpl[6], ep, false);
+        int actp[NI];
+        Row<T> rowsp[NROW];
+        row_values(k, zpl, ep, dp, actp, rowsp);
+      }
+      for (int j = 0; j < NI; ++j) {
+        if (!act[j]) continue;
+        T st = W(k, sf(cur) + j) + alpha * W(k, WF::DS + j);
+        if (soc) st += d[j] - dp[j];
+        if (!(st > T(0))) ok = false;
+        W(k, sf(nb) + j) = st;
+        th_t += mr_abs(d[j] - st);
+        lg += mr_log(st > T(0) ? st : T(1));
+      }
+      fv += stage_cost(P, I, k, zt, e, sc, (T*)nullptr, (T*)nullptr);
+      if (lane_active(P, k)) fv += sc * P.lane_pen * zt[14];
+      if (k < N) {
+        T xn[NX];
+        faug<T, MODEL>(P, k, zt, xn);
+        if (soc) {
+          for (int i = 0; i < NX; ++i) zroll[i] = xn[i];
+        } else {
+          for (int i = 0; i < NX; ++i) {
+            T xt = W(k + 1, zf(cur) + i) + alpha * W(k + 1, WF::DZ + i);
+            th_t += mr_abs(xn[i] - xt);
+          }
+        }
+      }
+      store_z(k, nb, zt);
+    }
+    ph_t = fv - mu * lg;
+    if (!(th_t == th_t) || !(ph_t == ph_t)) ok = false;
+    return ok;
+  }
+
+  MR_HD bool filter_ok(T th, T ph) const {
+    for (int i = 0; i < FMAX; ++i)
+      if (i < nfilt && th >= filt_th[i] && ph >= filt_ph[i]) return false;
+    return true;
+  }
+  MR_HD void filter_add(T th, T ph) {
+    if (nfilt < FMAX) {
+      filt_th[nfilt] = th;
+      filt_ph[nfilt] = ph;
+      nfilt++;
+    } else {  // drop the oldest entry
+      for (int i = 0; i < FMAX - 1; ++i) { filt_th[i] = filt_th[i + 1]; filt_ph[i] = filt_ph[i + 1]; }
+      filt_th[FMAX - 1] = th;
+      filt_ph[FMAX - 1] = ph;
+    }
+  }
+
+  MR_HD T lane_violation() const {
+    T v = T(0);
+    if (!P.lane) return v;
+    for (int k = 1; k <= N; ++k) v = mr_max(v, W(k, zf(cur) + 14));
+    return v;
+  }
+
+  // ---------------- the IPM loop ----------------
+  MR_HD SolveOut solve() {
+    const T kappa_eps = T(10), kappa_mu = T(0.2), theta_mu = T(1.5);
+    const T mu_min = P.tol / T(10);
+    const T s_phi = T(2.3), s_theta = T(1.1), delta_sw = T(1), eta = T(1e-4), g_th = T(1e-5), g_ph = T(1e-5);
+    SolveOut out{2, 0, 0.0, 0.0};
+    T mu_prev = mu;
+    int acc_count = 0;
+    int it = 0;
+    for (it = 0;; ++it) {
+      eval_sweep(mu_prev);
+      T kkt = kkt_error(T(0));
+      out.kkt = (double)kkt;
+      out.obj = (double)(fval / sc);
+      if (!(kkt == kkt) || !(fval == fval)) { out.status = 3; break; }
+      if (kkt <= P.tol) { out.status = 0; break; }
+      if (P.acc_iter > 0) {
+        acc_count = (kkt <= P.acc_tol) ? acc_count + 1 : 0;
+        if (acc_count >= P.acc_iter) { out.status = 1; break; }
+      }
+      if (it >= P.max_iter) { out.status = 2; break; }
+      T mu_old = mu;
+      while (kkt_error(mu) <= kappa_eps * mu && mu > mu_min) {
+        T m1 = kappa_mu * mu, m2 = mr_exp(theta_mu * mr_log(mu));
+        mu = mr_max(mu_min, mr_min(m1, m2));
+      }
+      if (mu != mu_old) nfilt = 0;
+      // inertia-corrected factorisation
+      T delta = T(0);
+      bool first = true, fact_ok = false;
+      for (int tries = 0; tries < 60; ++tries) {
+        if (riccati(delta)) { fact_ok = true; break; }
+        if (first) {
+          delta = delta_last == T(0) ? T(1e-4) : mr_max(T(1e-20), delta_last / T(3));
+          first = false;
+        } else {
+          delta *= (delta_last == T(0) ? T(100) : T(8));
+        }
+        if (delta > T(1e40)) break;
+      }
+      if (!fact_ok) { out.status = 3; break; }
+      if (delta > T(0)) delta_last = delta;
+      T ap, ad, gphi;
+      forward(ap, ad, gphi);
+      // filter line search
+      const T th = theta, ph = fval - mu * logs;
+      const T th_pow = mr_exp(s_theta * mr_log(mr_max(th, T(1e-30))));
+      T a_min;
+      if (gphi < T(0)) {
+        T t1 = g_ph * th / (-gphi);
+        T t2 = delta_sw * th_pow / mr_exp(s_phi * mr_log(-gphi));
+        a_min = T(0.05) * mr_min(g_th, mr_min(t1, t2));
+      } else {
+        a_min = T(0.05) * g_th;
+      }
+      T alpha = ap;
+      bool accepted = false, ftype = false;
+      int nls = 0;
+      while (alpha >= a_min) {
+        for (int pass = 0; pass < 2 && !accepted; ++pass) {
+          bool soc = pass == 1;
+          T th_t, ph_t;
+          bool ok = trial(alpha, soc, th_t, ph_t);
+          if (ok) ok = th_t <= theta_max && filter_ok(th_t, ph_t);
+          if (ok) {
+            bool sw = gphi < T(0) && alpha * mr_exp(s_phi * mr_log(-gphi)) > delta_sw * th_pow;
+            if (th <= theta_min && sw) {
+              ok = ph_t <= ph + eta * alpha * gphi + T(1e-14) * mr_abs(ph);
+              ftype = true;
+            } else {
+              ok = th_t <= (T(1) - g_th) * th || ph_t <= ph - g_ph * th + T(1e-14) * mr_abs(ph);
+              ftype = false;
+            }
+          }
+          if (ok) { accepted = true; break; }
+          // second-order correction only after the first rejected trial with theta not decreased
+          if (!(nls == 0 && !soc && th_t >= th)) break;
+        }
+        if (accepted) break;
+        alpha *= T(0.5);
+        nls++;
+      }
+      if (!accepted) {
+        alpha = mr_max(alpha, a_min);
+        T th_t, ph_t;
+        trial(alpha, false, th_t, ph_t);
+        ftype = false;
+      }
+      if (!ftype) filter_add((T(1) - g_th) * th, ph - g_ph * th);
+      alpha_p = alpha;
+      alpha_d = ad;
+      mu_prev = mu;
+      cur = 1 - cur;
+    }
+    out.iters = it;
+    return out;
+  }
+};
+
+}  // namespace mr

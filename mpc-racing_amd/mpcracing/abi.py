@@ -1,0 +1,80 @@
+"""ctypes mirror of ``include/mpcracing.h`` (the C ABI of libmpcracing.so)."""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.abspath(os.path.join(HERE, "..", "csrc"))
+PRODUCT_LIB = os.path.join(CSRC, "libmpcracing.so")
+HOST_TWIN_LIB = os.path.join(CSRC, "libmpcracing_host.so")
+
+MR_MODEL = {"kin": 0, "dyn": 1, "blend": 2, "blend_pacejka": 3, "dyn_pacejka": 4}
+MR_PREC = {"fp64": 0, "fp32": 1}
+STATUS = {0: "solved", 1: "acceptable", 2: "max_iter", 3: "failed", 4: "lane_infeasible"}
+
+_I32 = ctypes.c_int32
+_D = ctypes.c_double
+_PD = ctypes.POINTER(ctypes.c_double)
+_PI32 = ctypes.POINTER(ctypes.c_int32)
+
+
+class MRConfig(ctypes.Structure):
+    _fields_ = [(n, _I32) for n in ("N", "model", "precision", "lane_bounds", "max_batch", "device",
+                                    "max_iter", "acceptable_iter")] + \
+               [(n, _D) for n in ("Ts", "tol", "acceptable_tol", "lane_penalty",
+                                  "lambda_s", "alpha_L", "min_steer", "max_steer", "min_throttle",
+                                  "max_steer_delta", "min_steer_delta", "max_throttle_delta",
+                                  "min_throttle_delta", "q_v_max", "v_max", "min_s_delta",
+                                  "m", "Iz", "lf", "lr", "Cf", "Cr", "T_max", "r_wheel", "C_wheel", "R",
+                                  "rho", "C_d", "A_f", "C_roll", "g", "max_steer_deg", "Vblendmin",
+                                  "Vblendmax")]
+
+
+class MRInputs(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("state0", "s0", "cx", "cy", "max_error", "runtime", "u_init")]
+
+
+class MROutputs(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("X", "U", "S", "eC", "eL", "status", "iters", "obj", "kkt")]
+
+
+# every symbol declared in include/mpcracing.h (checked by tests/test_abi.py)
+EXPORTS = ["mr_version", "mr_last_error", "mr_config_default", "mr_create", "mr_destroy", "mr_set_tyres",
+           "mr_solve_batch", "mr_workspace_bytes_per_instance"]
+
+
+def _bind_product(lib):
+    lib.mr_version.restype = ctypes.c_int
+    lib.mr_last_error.restype = ctypes.c_char_p
+    lib.mr_config_default.argtypes = [ctypes.POINTER(MRConfig)]
+    lib.mr_create.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(MRConfig)]
+    lib.mr_destroy.argtypes = [ctypes.c_void_p]
+    lib.mr_set_tyres.argtypes = [ctypes.c_void_p, _PD, _D, _PD, _D]
+    lib.mr_solve_batch.argtypes = [ctypes.c_void_p, _I32, ctypes.POINTER(MRInputs), ctypes.POINTER(MROutputs),
+                                   ctypes.c_void_p]
+    lib.mr_workspace_bytes_per_instance.argtypes = [ctypes.c_void_p]
+    lib.mr_workspace_bytes_per_instance.restype = ctypes.c_int64
+    return lib
+
+
+_product = None
+
+
+def load_product(path=PRODUCT_LIB):
+    """Load the gfx950 library. There is no fallback: a missing library is an error."""
+    global _product
+    if _product is None:
+        if not os.path.exists(path):
+            raise RuntimeError(f"libmpcracing.so not built ({path}); run `python __graft_entry__.py build`")
+        _product = _bind_product(ctypes.CDLL(path))
+    return _product
+
+
+def load_host_twin(path=HOST_TWIN_LIB):
+    """TEST-ONLY host build of the same solver source (never used by the product path)."""
+    lib = ctypes.CDLL(path)
+    lib.mrh_config_default.argtypes = [ctypes.POINTER(MRConfig)]
+    lib.mrh_solve_batch.argtypes = [ctypes.POINTER(MRConfig), _PD, _D, _PD, _D, ctypes.c_int,
+                                    ctypes.POINTER(MRInputs), ctypes.POINTER(MROutputs), ctypes.c_int]
+    lib.mrh_eval_dynamics.argtypes = [ctypes.POINTER(MRConfig), _PD, _D, _PD, _D, _PD, _PD, _PD, _PD, _PD, _PD]
+    lib.mrh_pacejka.argtypes = [_PD, _D, _D, ctypes.c_int, _PD]
+    return lib
