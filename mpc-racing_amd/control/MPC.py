@@ -1,0 +1,193 @@
+"""Drop-in ``control.MPC.MPC``: the reference's contouring MPC, solved on MI355X.
+
+Reference boundary (AlexGisi/mpc-racing control/MPC.py:10-22, :183-184): the
+constructor builds AND solves the NLP; ``solution()`` returns ``(sol, ret, dual)``
+with ``ret = (States 6x(N+1), U 2xN, S_hat (N+1,), e_hat_C[0..N-1], e_hat_L[0..N-1])``.
+This class keeps that signature and result layout and runs the solve as a
+batch of one on the GPU through libmpcracing.so (``mpcracing.batch``).
+``MPCBatch`` is the batched entry point used for throughput.
+
+Differences that are visible to a caller:
+  * ``sol`` is a ``SolveInfo`` record (truthy) instead of a CasADi OptiSol; it is
+    ``None`` when the solve did not converge, as in the reference's except branch
+    (:172-181) -- but no ``breakpoint()`` is hit and ``ret`` holds the last iterate.
+  * ``dual`` is ``None`` (the reference returns Opti's lam_g; callers only feed it
+    back as the ignored ``duals`` argument).
+  * the solver is a primal-dual interior-point method with IPOPT's rules, run to
+    tol 1e-8 (the reference's IPOPT tol is 1e-4).
+"""
+from dataclasses import dataclass
+import math
+
+import numpy as np
+
+from control.ControllerParameters import FixedControllerParameters, RuntimeControllerParameters
+from control.util import deg2rad
+from models.VehicleParameters import VehicleParameters, config_fields
+
+_solvers = {}
+
+
+@dataclass
+class SolveInfo:
+    status: str
+    iterations: int
+    objective: float
+    kkt_error: float
+
+    def __bool__(self):
+        return True
+
+
+def _fixed_fields(fp):
+    return dict(lambda_s=fp.lambda_s, alpha_L=fp.alpha_L, min_steer=fp.min_steer, max_steer=fp.max_steer,
+                min_throttle=fp.min_throttle, max_steer_delta=fp.max_steer_delta,
+                min_steer_delta=fp.min_steer_delta, max_throttle_delta=fp.max_throttle_delta,
+                min_throttle_delta=fp.min_throttle_delta, q_v_max=fp.q_v_max, v_max=fp.v_max,
+                max_iter=int(FixedControllerParameters.max_iter))
+
+
+def get_solver(N, Ts, model="dyn", lane_bounds=False, precision="fp64", max_batch=1, device=0, tyres=None):
+    """Cached BatchSolver for one NLP configuration (the reference rebuilds its NLP every call;
+    here the handle and its workspace are reused, only the data changes)."""
+    from mpcracing.batch import BatchSolver
+    fp = FixedControllerParameters()
+    key = (int(N), float(Ts), model, bool(lane_bounds), precision, int(max_batch), int(device),
+           tuple(sorted(config_fields().items())), tuple(sorted(_fixed_fields(fp).items())),
+           None if tyres is None else repr(tyres))
+    s = _solvers.get(key)
+    if s is None:
+        s = BatchSolver(N, model, precision, lane_bounds, Ts, max_batch=max_batch, device=device, tyres=tyres,
+                        **config_fields(), **_fixed_fields(fp))
+        _solvers[key] = s
+    return s
+
+
+class MPCBatch:
+    """Solve B MPC instances at once.  Arrays follow include/mpcracing.h (instance index last)."""
+
+    def __init__(self, N, Ts=None, model="dyn", lane_bounds=False, precision="fp64", max_batch=1024, device=0,
+                 tyres=None):
+        Ts = FixedControllerParameters.Ts if Ts is None else Ts
+        self.N = int(N)
+        self.solver = get_solver(N, Ts, model, lane_bounds, precision, max_batch, device, tyres)
+
+    def solve(self, state0, s0, cx, cy, max_error, runtime, u_init=None):
+        out = self.solver.solve(dict(state0=state0, s0=s0, cx=cx, cy=cy, max_error=max_error, runtime=runtime,
+                                     u_init=u_init))
+        return out
+
+
+class MPC:
+    def __init__(self, state0, s0, centerline_x_poly_coeffs, centerline_y_poly_coeffs, max_error,
+                 runtime_params, sol0=None, duals=None, last_controls=None, Ts=None, N=None, *,
+                 model="dyn", lane_bounds=False, device=0):
+        # sol0 / duals are accepted and ignored, as in the reference (MPC.py:17-18)
+        self.fixed_params = FixedControllerParameters()
+        self.runtime_params = runtime_params
+        self.state0 = state0
+        N = self.fixed_params.N if N is None else int(N)
+        Ts = FixedControllerParameters.Ts if Ts is None else float(Ts)
+        self.N, self.Ts = N, Ts
+        if last_controls is not None:
+            # initial guess = last_controls shifted by one, last repeated (MPC.py:120-121)
+            lc = list(last_controls)
+            shifted = lc[1:] + [lc[-1]]
+            u_init = np.array(shifted, dtype=np.float64).T.reshape(2, N, 1)
+        else:
+            if state0.throttle is None or state0.steer is None:
+                raise ValueError("MPC needs state0.throttle/steer or last_controls for its initial guess "
+                                 "(control/MPC.py:123)")
+            u_init = None
+        batch = dict(
+            state0=np.array(state0.as_state0_row() if hasattr(state0, "as_state0_row") else _state_row(state0),
+                            dtype=np.float64).reshape(8, 1),
+            s0=np.array([float(s0)]),
+            cx=np.array(centerline_x_poly_coeffs, dtype=np.float64).reshape(5, 1),
+            cy=np.array(centerline_y_poly_coeffs, dtype=np.float64).reshape(5, 1),
+            max_error=np.array([float(max_error)]),
+            runtime=np.array(_runtime_row(runtime_params), dtype=np.float64).reshape(5, 1),
+            u_init=u_init,
+        )
+        solver = get_solver(N, Ts, model, lane_bounds, device=device)
+        out = {k: v.cpu().numpy() for k, v in solver.solve(batch).items()}
+        status = int(out["status"][0])
+        from mpcracing.abi import STATUS
+        info = SolveInfo(STATUS.get(status, str(status)), int(out["iters"][0]), float(out["obj"][0]),
+                         float(out["kkt"][0]))
+        self.info = info
+        self.ret = (out["X"][:, :, 0], out["U"][:, :, 0], out["S"][:, 0],
+                    [float(v) for v in out["eC"][:, 0]], [float(v) for v in out["eL"][:, 0]])
+        if status in (0, 1):
+            self.sol = info
+        else:
+            print(f"MPC solve did not converge: {info.status} after {info.iterations} iterations")
+            self.sol = None
+        self.dual = None
+
+    def solution(self):
+        return self.sol, self.ret, self.dual
+
+    def solve(self):
+        """Alias of ``solution()`` (the solve itself ran in the constructor, as in the reference)."""
+        return self.solution()
+
+    # numeric versions of the model pieces the reference exposes as methods (MPC.py:186-283)
+    def f_vehicle(self, x_k, u_k, Ts):
+        return _f_vehicle(np.asarray(x_k, dtype=np.float64), np.asarray(u_k, dtype=np.float64), Ts)
+
+    def f_vehicle_kinematic(self, x_k, u_k, Ts):
+        return _f_vehicle_kinematic(np.asarray(x_k, dtype=np.float64), np.asarray(u_k, dtype=np.float64), Ts)
+
+    def steer_cmd_to_angle(self, steer_cmd, v_x, v_y):
+        vel = math.sqrt(v_x ** 2 + v_y ** 2) * 3.6
+        gain = -0.001971664699 * vel + 0.986547
+        return deg2rad(steer_cmd * gain * VehicleParameters.max_steer)
+
+    def Fx(self, throttle, v_x):
+        V = VehicleParameters
+        rpm = (v_x / V.C_wheel) * 60 * V.R * 4.5
+        eta = -0.00004428225806 * rpm + 1.282413306
+        return (throttle * eta * V.T_max * V.R / V.r_wheel - 0.5 * V.rho * V.C_d * V.A_f * v_x ** 2
+                - V.C_roll * V.m * V.g)
+
+
+def _state_row(s):
+    nan = math.nan
+    return [s.x, s.y, s.yaw, s.v_x, s.v_y, s.yaw_dot, nan if s.throttle is None else s.throttle,
+            nan if s.steer is None else s.steer]
+
+
+def _runtime_row(rp):
+    if hasattr(rp, "as_runtime_row"):
+        return rp.as_runtime_row()
+    return [rp.alpha_c, RuntimeControllerParameters.d_max, rp.q_v_y, rp.n, rp.beta_delta]
+
+
+def _f_vehicle(x, u, Ts):
+    V = VehicleParameters
+    m = MPC.__new__(MPC)
+    X, Y, yaw, vx, vy, r = x[:6]
+    F = m.Fx(u[0], vx)
+    d = m.steer_cmd_to_angle(u[1], vx, vy)
+    tf = math.atan2(vy + V.lf * r, vx + 0.1)
+    tr = math.atan2(vy - V.lr * r, vx + 0.1)
+    Fyf = V.Cf * (d - tf)
+    Fyr = V.Cr * (-tr)
+    vxd = (F - Fyf * math.sin(d)) / V.m + vy * r
+    vyd = (Fyf * math.cos(d) + Fyr) / V.m - vx * r
+    rd = (Fyf * math.cos(d) * V.lf - Fyr * V.lr) / V.Iz
+    return np.array([X + (vx * math.cos(yaw) - vy * math.sin(yaw)) * Ts,
+                     Y + (vx * math.sin(yaw) + vy * math.cos(yaw)) * Ts,
+                     yaw + r * Ts, vx + vxd * Ts, vy + vyd * Ts, r + rd * Ts])
+
+
+def _f_vehicle_kinematic(x, u, Ts):
+    V = VehicleParameters
+    m = MPC.__new__(MPC)
+    X, Y, yaw, vx, vy, r = x[:6]
+    F = m.Fx(u[0], vx)
+    d = m.steer_cmd_to_angle(u[1], vx, vy)
+    return np.array([X + (vx * math.cos(yaw) - vy * math.sin(yaw)) * Ts,
+                     Y + (vx * math.sin(yaw) + vy * math.cos(yaw)) * Ts,
+                     yaw + r * Ts, vx + F / V.m * Ts, r * V.lr, vx / (V.lr + V.lf) * math.tan(d)])

@@ -25,6 +25,9 @@
 #pragma once
 #include "mr_common.h"
 #include "gen_dynamics.h"
+#ifndef MR_PROF
+#define MR_PROF(slot, stmt) stmt
+#endif
 
 namespace mr {
 
@@ -989,7 +992,7 @@ struct Solver {
     int acc_count = 0;
     int it = 0;
     for (it = 0;; ++it) {
-      eval_sweep(mu_prev);
+      MR_PROF(0, eval_sweep(mu_prev));
       T kkt = kkt_error(T(0));
       out.kkt = (double)kkt;
       out.obj = (double)(fval / sc);
@@ -1010,7 +1013,9 @@ struct Solver {
       T delta = T(0);
       bool first = true, fact_ok = false;
       for (int tries = 0; tries < 60; ++tries) {
-        if (riccati(delta)) { fact_ok = true; break; }
+        bool rok;
+        MR_PROF(1, rok = riccati(delta));
+        if (rok) { fact_ok = true; break; }
         if (first) {
           delta = delta_last == T(0) ? T(1e-4) : mr_max(T(1e-20), delta_last / T(3));
           first = false;
@@ -1022,7 +1027,7 @@ struct Solver {
       if (!fact_ok) { out.status = 3; break; }
       if (delta > T(0)) delta_last = delta;
       T ap, ad, gphi;
-      forward(ap, ad, gphi);
+      MR_PROF(2, forward(ap, ad, gphi));
       // filter line search
       const T th = theta, ph = fval - mu * logs;
       const T th_pow = mr_exp(s_theta * mr_log(mr_max(th, T(1e-30))));
@@ -1041,7 +1046,8 @@ struct Solver {
         for (int pass = 0; pass < 2 && !accepted; ++pass) {
           bool soc = pass == 1;
           T th_t, ph_t;
-          bool ok = trial(alpha, soc, th_t, ph_t);
+          bool ok;
+          MR_PROF(3, ok = trial(alpha, soc, th_t, ph_t));
           if (ok) ok = th_t <= theta_max && filter_ok(th_t, ph_t);
           if (ok) {
             bool sw = gphi < T(0) && alpha * mr_exp(s_phi * mr_log(-gphi)) > delta_sw * th_pow;

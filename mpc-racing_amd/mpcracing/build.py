@@ -1,0 +1,45 @@
+"""In-tree builds of the native libraries (no JIT cache: the .so files travel with the repo).
+
+* libmpcracing.so       -- the product: gfx950 kernels + C ABI (hipcc --offload-arch=gfx950)
+* libmpcracing_host.so  -- TEST-ONLY g++ build of the same solver source (CPU test suite)
+"""
+import os
+import subprocess
+
+from .abi import CSRC, PRODUCT_LIB, HOST_TWIN_LIB
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+SOURCES = ["mpcracing.hip", "mr_batch.h", "mr_solver.h", "mr_common.h", "gen_dynamics.h"]
+INCLUDE = os.path.abspath(os.path.join(CSRC, "..", "..", "include"))
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_hip(force=False, verbose=True):
+    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(INCLUDE, "mpcracing.h")]
+    if not force and not _stale(PRODUCT_LIB, deps):
+        return PRODUCT_LIB
+    cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
+           "-o", PRODUCT_LIB, os.path.join(CSRC, "mpcracing.hip")]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return PRODUCT_LIB
+
+
+def build_host_twin(force=False, verbose=True):
+    deps = [os.path.join(CSRC, s) for s in ["mpcracing_host.cpp"] + SOURCES[1:]] + \
+           [os.path.join(INCLUDE, "mpcracing.h")]
+    if not force and not _stale(HOST_TWIN_LIB, deps):
+        return HOST_TWIN_LIB
+    cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-o", HOST_TWIN_LIB,
+           os.path.join(CSRC, "mpcracing_host.cpp")]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return HOST_TWIN_LIB

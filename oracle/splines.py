@@ -152,7 +152,7 @@ class Centerline:
         right_min = 10000
         for q in np.arange(s_round, s + la, 0.5):
             key = r2(q % self.length)
-            left, right = self.err[key]  # KeyError past the table end, as pandas .loc
+            left, right = self.err[key]  # pandas .loc row lookup
             if left < left_min:
                 left_min = left
             if right < right_min:

@@ -1,0 +1,186 @@
+"""CPU checks of the product's solver source through its host (g++) build:
+generated analytic derivatives vs torch autograd of the oracle dynamics, the
+Pacejka jets, and full solves vs the oracle NLP solver (small cases)."""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import host_twin as ht
+from mpcracing import workload as wl
+from oracle import dynamics as dyn
+from oracle.nlp import MPCProblem, solve_ipm, pacejka_torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GJ = json.load(open(os.path.join(HERE, "golden", "golden.json")))
+TY = GJ["tyres"]["pacejka-2"]
+TYRES = ((TY["front_tire.a"], TY["front_tire.Fz"][0]), (TY["back_tire.a"], TY["back_tire.Fz"][0]))
+P = lambda a: np.ascontiguousarray(a, np.float64).ctypes.data_as(ctypes.POINTER(ctypes.c_double))  # noqa: E731
+
+
+def _torch_model(model):
+    M = dyn._torch_ns()
+    tyres = None
+    if "pacejka" in model:
+        tyres = (pacejka_torch(*TYRES[0]), pacejka_torch(*TYRES[1]))
+
+    def f(v, Ts=0.05):
+        x, u = [v[i] for i in range(6)], [v[6], v[7]]
+        if model == "kin":
+            return dyn.f_vehicle_kinematic(x, u, Ts, M)
+        fd = dyn.f_vehicle(x, u, Ts, M, tyres)
+        if model in ("dyn", "dyn_pacejka"):
+            return fd
+        fk = dyn.f_vehicle_kinematic(x, u, Ts, M)
+        vel = torch.sqrt(v[3] ** 2 + v[4] ** 2)
+        lo, hi = dyn.VP.Vblendmin, dyn.VP.Vblendmax
+        lam = torch.where(vel <= lo, torch.zeros_like(vel),
+                          torch.where(vel >= hi, torch.ones_like(vel), (vel - lo) / (hi - lo)))
+        return lam * fd + (1 - lam) * fk
+    return f
+
+
+@pytest.mark.parametrize("model", ["kin", "dyn", "blend", "blend_pacejka", "dyn_pacejka"])
+def test_generated_derivatives_match_autograd(model):
+    rng = np.random.default_rng(7)
+    c = ht.config(20, model)
+    f = _torch_model(model)
+    for trial in range(12):
+        vx = [1.5, 8.0, 25.0][trial % 3]  # kinematic / blend / dynamic regions of the blended law
+        x = np.array([rng.normal(100, 50), rng.normal(-20, 50), rng.uniform(-3, 3), vx,
+                      rng.normal(0, 1), rng.normal(0, 0.5)])
+        u = np.array([rng.uniform(-1, 0.85), rng.uniform(-0.9, 0.9)])
+        nu = rng.normal(0, 10, 6)
+        fo, J, H = np.zeros(6), np.zeros(48), np.zeros(36)
+        tyr = TYRES if "pacejka" in model else None
+        rc = ht.lib().mrh_eval_dynamics(ctypes.byref(c), P(tyr[0][0]) if tyr else None, tyr[0][1] if tyr else 0.0,
+                                        P(tyr[1][0]) if tyr else None, tyr[1][1] if tyr else 0.0,
+                                        P(x), P(u), P(nu), fo.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                        J.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                        H.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+        assert rc == 0
+        v = torch.tensor(np.concatenate([x, u]))
+        fr = f(v).numpy()
+        Jr = torch.func.jacrev(f)(v).numpy()
+        Hr = torch.func.hessian(lambda w: torch.dot(torch.tensor(nu), f(w)))(v).numpy()
+        Hp = np.zeros((8, 8))
+        q = 0
+        for a in range(8):
+            for b in range(a, 8):
+                Hp[a, b] = Hp[b, a] = H[q]
+                q += 1
+        np.testing.assert_allclose(fo, fr, rtol=1e-13, atol=1e-11)
+        np.testing.assert_allclose(J.reshape(6, 8), Jr, rtol=1e-10, atol=1e-10)
+        np.testing.assert_allclose(Hp, Hr, rtol=1e-8, atol=1e-8 * max(1.0, np.abs(Hr).max()))
+
+
+@pytest.mark.parametrize("coef", ["pacejka-1", "pacejka-2", "vehicle_default_Fz1"])
+def test_pacejka_jet(coef):
+    if coef == "vehicle_default_Fz1":
+        # the initial coefficients of learning/vehicle.py:75 at a small load: |B*alpha| ~ 1 exercises
+        # the non-series branch
+        a, Fz = [1.3, -22.1, 1011, 1078, 1.82, 0.208, 0.0, -0.354, 0.707], 1.0
+    else:
+        t = GJ["tyres"][coef]
+        a, Fz = t["front_tire.a"], t["front_tire.Fz"][0]
+    fy = pacejka_torch(a, Fz)
+    for al in [-0.3, -0.02, 1e-5, 0.07, 0.25]:
+        out = np.zeros(3)
+        ht.lib().mrh_pacejka(P(a), Fz, al, 0, out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+        t = torch.tensor(al, dtype=torch.float64)
+        d1 = torch.func.grad(fy)(t)
+        d2 = torch.func.grad(torch.func.grad(fy))(t)
+        ref = np.array([float(fy(t)), float(d1), float(d2)])
+        np.testing.assert_allclose(out, ref, rtol=1e-9, atol=1e-9 * max(1.0, abs(ref[1])))
+        out32 = np.zeros(3)
+        ht.lib().mrh_pacejka(P(a), Fz, al, 1, out32.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+        assert abs(out32[0] - ref[0]) <= 2e-6 * max(1.0, abs(ref[0]))  # fp32 form is usable (naive is not)
+
+
+def _compare(name, n, tol=1e-10, parity=1e-6):
+    cfg = wl.CONFIGS[name]
+    b = wl.make_batch(name, limit=n)
+    c = ht.config(cfg["N"], cfg["model"], "fp64", cfg["lane"], cfg["Ts"], tol=tol)
+    tyres = wl.tyre_coeffs(cfg["tyres"]) if cfg["tyres"] else None
+    out = ht.solve(c, b, tyres=tyres)
+    assert (out["status"] == 0).all(), out["status"]
+    for i, inst in enumerate(wl.instance_dicts(b)):
+        p = MPCProblem(inst["state0"], inst["s0"], inst["cx"], inst["cy"], inst["max_error"], N=cfg["N"],
+                       Ts=cfg["Ts"], model=cfg["model"], lane_bounds=cfg["lane"], tyres=tyres,
+                       elastic=1e5 if cfg["lane"] else None)
+        r = solve_ipm(p, tol=1e-10)
+        assert r.status == 0
+        X, U, S, eC, eL = p.unpack(r.w)
+        dU = np.abs(U - out["U"][:, :, i])
+        dU[0, -1] = 0.0  # last throttle: cost-insensitive direction, fixed by the barrier only
+        assert dU.max() < parity, (i, dU.max())
+        assert np.abs(X[:, :-1] - out["X"][:, :-1, i]).max() < parity
+        assert np.abs(np.delete(X[:, -1], 3) - np.delete(out["X"][:, -1, i], 3)).max() < parity
+        assert np.abs(S - out["S"][:, i]).max() < parity
+        assert np.abs(eC - out["eC"][:, i]).max() < parity and np.abs(eL - out["eL"][:, i]).max() < parity
+        assert abs(r.obj - out["obj"][i]) <= 1e-8 * max(1.0, abs(r.obj))
+
+
+def test_config1_dynamic_and_kinematic_vs_oracle():
+    """C1: script/test_mpc.py inputs (N = 20, Ts = 0.1), reference dynamic NLP and kinematic variant."""
+    b = wl.make_batch("C1")
+    inst = wl.instance_dicts(b)[0]
+    for model in ("dyn", "kin"):
+        c = ht.config(20, model, "fp64", False, 0.1, tol=1e-10)
+        out = ht.solve(c, b)
+        assert out["status"][0] == 0
+        p = MPCProblem(inst["state0"], inst["s0"], inst["cx"], inst["cy"], inst["max_error"], N=20, Ts=0.1,
+                       model=model)
+        r = solve_ipm(p, tol=1e-10)
+        X, U, S, eC, eL = p.unpack(r.w)
+        dU = np.abs(U - out["U"][:, :, 0])
+        dU[0, -1] = 0.0
+        assert dU.max() < 1e-6 and np.abs(S - out["S"][:, 0]).max() < 1e-6
+        # the wrap-around rate row of MPC.py:142-143 is active at this solution: U1_0 - U1_{N-1} = 0.2
+        assert abs((out["U"][1, 0, 0] - out["U"][1, -1, 0]) - 0.2) < 1e-6
+
+
+def test_c2_kinematic_vs_oracle():
+    _compare("C2", 3)
+
+
+@pytest.mark.slow
+def test_c4_blended_fp64_vs_oracle():
+    _compare("C4", 2)
+
+
+@pytest.mark.slow
+def test_c3_lane_rows_vs_oracle():
+    # elastic lane rows (exact penalty) in the product and in the oracle; t* = 0 at these solutions
+    _compare("C3", 2)
+
+
+@pytest.mark.slow
+def test_elastic_lane_rows_equal_hard_rows():
+    """Where the oracle's IPM converges on the hard rows, the elastic NLP has the same KKT point."""
+    cfg = wl.CONFIGS["C3"]
+    b = wl.make_batch("C3", limit=3)
+    inst = wl.instance_dicts(b)[2]
+    res = []
+    for el in (None, 1e5):
+        p = MPCProblem(inst["state0"], inst["s0"], inst["cx"], inst["cy"], inst["max_error"], N=cfg["N"],
+                       Ts=cfg["Ts"], model=cfg["model"], lane_bounds=True, elastic=el)
+        r = solve_ipm(p, tol=1e-10)
+        assert r.status == 0
+        res.append(p.unpack(r.w))
+    assert np.abs(res[0][1] - res[1][1])[:, :-1].max() < 1e-7
+
+
+def test_fp32_close_to_fp64():
+    cfg = wl.CONFIGS["C4"]
+    b = wl.make_batch("C4", limit=16)
+    o64 = ht.solve(ht.config(40, "blend", "fp64", tol=1e-8), b)
+    o32 = ht.solve(ht.config(40, "blend", "fp32", tol=1e-4, acceptable_iter=15, acceptable_tol=1e-3), b)
+    ok = (o64["status"] == 0) & (o32["status"] <= 1)
+    assert ok.mean() >= 0.9
+    # fp32 solutions track the fp64 ones (stated tolerance 5e-2 on controls, 0.5 m on states)
+    dU = np.abs(o32["U"] - o64["U"])[:, :-1, ok]
+    assert np.median(dU) < 1e-3 and dU.max() < 5e-2 * 10
