@@ -99,6 +99,10 @@ typedef struct mr_outputs {
   int32_t* iters;  /* [B] interior-point iterations */
   double* obj;     /* optional [B] objective value (NULL to skip) */
   double* kkt;     /* optional [B] final scaled KKT error (NULL to skip) */
+  double* trace;   /* optional [trace_cap][8] per-iteration record of instance trace_instance:
+                      kkt, mu, alpha_primal, alpha_dual, delta (inertia), theta, phi, line-search trials */
+  int32_t trace_instance;
+  int32_t trace_cap;
 } mr_outputs;
 
 typedef struct mr_handle mr_handle;
@@ -112,6 +116,12 @@ int mr_destroy(mr_handle* h);
    (state dict keys front_tire.a / front_tire.Fz / back_tire.a / back_tire.Fz). */
 int mr_set_tyres(mr_handle* h, const double* a_front, double Fz_front, const double* a_back, double Fz_back);
 int mr_solve_batch(mr_handle* h, int32_t B, const mr_inputs* in, mr_outputs* out, void* hip_stream);
+/* Diagnostics: the handle's vehicle dynamics (fp64) at n points, device arrays x [n][6], u [n][2],
+   nu [n][6] -> f [n][6], J [n][6*8] (d f / d(x, u)), H [n][36] (packed upper triangle of
+   sum_i nu_i d2 f_i / d(x, u)^2); J == NULL evaluates the value-only variant into f.
+   Replaces CasADi's evaluation of f_vehicle (control/MPC.py:186-229). */
+int mr_eval_dynamics(mr_handle* h, int32_t n, const double* x, const double* u, const double* nu, double* f,
+                     double* J, double* H, void* hip_stream);
 /* workspace bytes used per instance for the handle's configuration */
 int64_t mr_workspace_bytes_per_instance(const mr_handle* h);
 

@@ -77,9 +77,39 @@ static int dispatch_model(mr_handle* h, int B, const mr_inputs* in, mr_outputs* 
   return fail(MR_ERR_ARG, "unknown model");
 }
 
+template <int MODEL>
+__global__ void mr_eval_dynamics_kernel(ProbParams<double> P, int n, const double* x, const double* u,
+                                        const double* nu, double* f, double* J, double* H) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (J == nullptr)  // value-only variant (used by the rollout / line search)
+    Dyn<double, MODEL>::f(P, x + 6 * i, u + 2 * i, f + 6 * i);
+  else
+    Dyn<double, MODEL>::fjh(P, x + 6 * i, u + 2 * i, nu + 6 * i, f + 6 * i, J + 48 * i, H + 36 * i);
+}
+
 extern "C" {
 
 int mr_version(void) { return 100; }
+
+int mr_eval_dynamics(mr_handle* h, int32_t n, const double* x, const double* u, const double* nu, double* f,
+                     double* J, double* H, void* hip_stream) {
+  if (!h || !x || !u || !f || n < 0 || (J && (!H || !nu))) return fail(MR_ERR_ARG, "null argument");
+  ProbParams<double> P;
+  fill_params<double>(h->cfg, h->tf, h->tr, P);
+  hipStream_t st = (hipStream_t)hip_stream;
+  dim3 grid((n + 63) / 64), block(64);
+  switch (h->cfg.model) {
+    case MR_MODEL_KINEMATIC: hipLaunchKernelGGL(mr_eval_dynamics_kernel<MODEL_KIN>, grid, block, 0, st, P, n, x, u, nu, f, J, H); break;
+    case MR_MODEL_DYNAMIC: hipLaunchKernelGGL(mr_eval_dynamics_kernel<MODEL_DYN>, grid, block, 0, st, P, n, x, u, nu, f, J, H); break;
+    case MR_MODEL_BLENDED: hipLaunchKernelGGL(mr_eval_dynamics_kernel<MODEL_BLEND>, grid, block, 0, st, P, n, x, u, nu, f, J, H); break;
+    case MR_MODEL_BLENDED_PACEJKA: hipLaunchKernelGGL(mr_eval_dynamics_kernel<MODEL_BLEND_PACEJKA>, grid, block, 0, st, P, n, x, u, nu, f, J, H); break;
+    case MR_MODEL_DYNAMIC_PACEJKA: hipLaunchKernelGGL(mr_eval_dynamics_kernel<MODEL_DYN_PACEJKA>, grid, block, 0, st, P, n, x, u, nu, f, J, H); break;
+    default: return fail(MR_ERR_ARG, "unknown model");
+  }
+  HIP_TRY(hipGetLastError());
+  return MR_OK;
+}
 
 const char* mr_last_error(void) { return g_err.c_str(); }
 

@@ -17,7 +17,8 @@ static void run(const mr_config& c, const TyreCoef<double>& tf, const TyreCoef<d
                 const mr_inputs& in, const mr_outputs& out, int nthreads) {
   ProbParams<T> P;
   fill_params<T>(c, tf, tr, P);
-  std::vector<T> ws((size_t)WF::NF * (c.N + 1) * (size_t)B);
+  // poisoned workspace: any read-before-write shows up as NaN (hipMalloc memory is not zeroed)
+  std::vector<T> ws((size_t)WF::NF * (c.N + 1) * (size_t)B, (T)NAN);
 #pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
   for (int i = 0; i < B; ++i) {
     WS<T> W{ws.data() + i, (int64_t)B};

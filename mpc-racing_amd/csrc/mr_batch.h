@@ -71,12 +71,13 @@ MR_HD SolveOut solve_instance(const ProbParams<T>& P, const mr_inputs& in, const
   if (I.n < 1) I.n = 1;
   I.beta = T(in.runtime[4 * B + i]);
   Solver<T, MODEL> S(P, I, W);
+  if (out.trace && out.trace_instance == i) { S.trace = out.trace; S.trace_cap = out.trace_cap; }
   S.init(in.u_init ? in.u_init + i : nullptr, B);
   SolveOut r = S.solve();
   // outputs (the ret tuple of control/MPC.py:166-171), back in global coordinates
   const int b = S.cur;
   for (int k = 0; k <= N; ++k) {
-    T z[NZ];
+    T z[NZS];
     S.load_z(k, b, z);
     out.X[(0 * (N + 1) + k) * B + i] = (double)z[0] + X0;
     out.X[(1 * (N + 1) + k) * B + i] = (double)z[1] + Y0;

@@ -438,6 +438,8 @@ struct Solver {
   // iteration aggregates (eval sweep)
   T stat_max, pr_max, theta, slam_max, slam_min, nu1, lam1, fval, logs;
   int me, mi;
+  double* trace = nullptr;  // optional per-iteration record (diagnostics)
+  int trace_cap = 0;
 
   MR_HD Solver(const ProbParams<T>& P_, const Inst<T>& I_, WS<T> W_) : P(P_), I(I_), W(W_), N(P_.N) {}
 
@@ -489,6 +491,10 @@ struct Solver {
       errors(I, z[0], z[1], z[6], e, false);
       z[14] = lane_active(P, k) ? mr_max(mr_abs(e.eC) - I.max_err, T(0)) + T(1e-2) : T(0);
       store_z(k, 0, z);
+#ifdef MR_DEBUG_PRINT
+      if (trace) printf("init k=%d vx=%g readback=%g X=%g S=%g\n", k, (double)z[3], (double)W(k, WF::Z0 + 3),
+                        (double)z[0], (double)z[6]);
+#endif
       // objective gradient for the gradient-based scaling (elastic variables excluded)
       T g[NZ];
       for (int i = 0; i < NZ; ++i) g[i] = T(0);
@@ -573,6 +579,11 @@ struct Solver {
           nu1 += mr_abs(v);
         }
         load_z(k + 1, cur, znext);
+#ifdef MR_DEBUG_PRINT
+        if (trace && mu_prev == T(0.1) && alpha_p == T(0))
+          printf("eval k=%d cur=%d z.vx=%g znext.vx=%g znext.X=%g\n", k, cur, (double)z[3], (double)znext[3],
+                 (double)znext[0]);
+#endif
       }
       T H[NH], g0[NZ], g1[NZ], gl[NZ], st[NZ];
       for (int i = 0; i < NH; ++i) H[i] = T(0);
@@ -993,6 +1004,15 @@ struct Solver {
     int it = 0;
     for (it = 0;; ++it) {
       MR_PROF(0, eval_sweep(mu_prev));
+      if (trace && it == 0 && trace_cap >= 100 + N + 1) {  // diagnostics: initial defects per stage
+        for (int k = 0; k < N; ++k) {
+          double* tr = trace + 8 * (100 + k);
+          for (int i = 0; i < 6; ++i) tr[i] = (double)W(k, WF::C + i);
+          tr[6] = (double)(mr_abs(W(k, WF::C + 6)) + mr_abs(W(k, WF::C + 7)) + mr_abs(W(k, WF::C + 8)) +
+                           mr_abs(W(k, WF::C + 9)) + mr_abs(W(k, WF::C + 10)));
+          tr[7] = (double)W(k + 1, zf(cur) + 3);
+        }
+      }
       T kkt = kkt_error(T(0));
       out.kkt = (double)kkt;
       out.obj = (double)(fval / sc);
@@ -1074,12 +1094,22 @@ struct Solver {
         ftype = false;
       }
       if (!ftype) filter_add((T(1) - g_th) * th, ph - g_ph * th);
+      if (trace && it < trace_cap) {
+        double* tr = trace + 8 * it;
+        tr[0] = (double)kkt; tr[1] = (double)mu; tr[2] = (double)alpha; tr[3] = (double)ad;
+        tr[4] = (double)delta; tr[5] = (double)th; tr[6] = (double)ph; tr[7] = (double)(accepted ? nls : -1);
+      }
       alpha_p = alpha;
       alpha_d = ad;
       mu_prev = mu;
       cur = 1 - cur;
     }
     out.iters = it;
+    if (trace && it < trace_cap) {  // final record: why the loop ended
+      double* tr = trace + 8 * it;
+      tr[0] = (double)out.kkt; tr[1] = (double)fval; tr[2] = (double)theta; tr[3] = (double)stat_max;
+      tr[4] = (double)pr_max; tr[5] = (double)sc; tr[6] = (double)mu; tr[7] = 1000.0 + out.status;
+    }
     return out;
   }
 };

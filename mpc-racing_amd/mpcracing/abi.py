@@ -34,12 +34,13 @@ class MRInputs(ctypes.Structure):
 
 
 class MROutputs(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_void_p) for n in ("X", "U", "S", "eC", "eL", "status", "iters", "obj", "kkt")]
+    _fields_ = [(n, ctypes.c_void_p) for n in ("X", "U", "S", "eC", "eL", "status", "iters", "obj", "kkt",
+                                               "trace")] + [("trace_instance", _I32), ("trace_cap", _I32)]
 
 
 # every symbol declared in include/mpcracing.h (checked by tests/test_abi.py)
 EXPORTS = ["mr_version", "mr_last_error", "mr_config_default", "mr_create", "mr_destroy", "mr_set_tyres",
-           "mr_solve_batch", "mr_workspace_bytes_per_instance"]
+           "mr_solve_batch", "mr_workspace_bytes_per_instance", "mr_eval_dynamics"]
 
 
 def _bind_product(lib):
@@ -51,6 +52,7 @@ def _bind_product(lib):
     lib.mr_set_tyres.argtypes = [ctypes.c_void_p, _PD, _D, _PD, _D]
     lib.mr_solve_batch.argtypes = [ctypes.c_void_p, _I32, ctypes.POINTER(MRInputs), ctypes.POINTER(MROutputs),
                                    ctypes.c_void_p]
+    lib.mr_eval_dynamics.argtypes = [ctypes.c_void_p, _I32] + [ctypes.c_void_p] * 7
     lib.mr_workspace_bytes_per_instance.argtypes = [ctypes.c_void_p]
     lib.mr_workspace_bytes_per_instance.restype = ctypes.c_int64
     return lib

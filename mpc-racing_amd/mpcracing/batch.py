@@ -82,7 +82,7 @@ class BatchSolver:
                 "iters": torch.empty(B, dtype=torch.int32, device=d),
                 "obj": torch.empty(B, **f), "kkt": torch.empty(B, **f)}
 
-    def launch(self, dev_in, out, stream=None):
+    def launch(self, dev_in, out, stream=None, trace_instance=-1):
         """Enqueue one batched solve on ``stream`` (default: torch's current stream); no sync."""
         B = int(dev_in["s0"].shape[0])
         N = self.N
@@ -97,17 +97,22 @@ class BatchSolver:
                                  f"{tuple(v.shape)} {v.dtype} {v.device}")
         ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
         inp = abi.MRInputs(*[ptr(dev_in.get(k)) for k in _IN_KEYS])
-        o = abi.MROutputs(*[ptr(out[k]) for k in ("X", "U", "S", "eC", "eL", "status", "iters", "obj", "kkt")])
+        tr = out.get("trace")
+        o = abi.MROutputs(*[ptr(out.get(k)) for k in ("X", "U", "S", "eC", "eL", "status", "iters", "obj", "kkt",
+                                                      "trace")], int(trace_instance),
+                          int(tr.shape[0]) if tr is not None else 0)
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
         self._check(self.lib.mr_solve_batch(self.h, B, ctypes.byref(inp), ctypes.byref(o),
                                             ctypes.c_void_p(st.cuda_stream)))
         return out
 
-    def solve(self, batch, stream=None):
+    def solve(self, batch, stream=None, trace_instance=-1, trace_cap=0):
         """Blocking solve of a host or device batch; returns device output tensors."""
         dev_in = self.to_device(batch)
         out = self.alloc_outputs(int(dev_in["s0"].shape[0]))
-        self.launch(dev_in, out, stream)
+        if trace_cap:
+            out["trace"] = torch.zeros((trace_cap, 8), dtype=torch.float64, device=self.device)
+        self.launch(dev_in, out, stream, trace_instance)
         torch.cuda.synchronize(self.device)
         return out
 

@@ -24,7 +24,12 @@ def build_hip(force=False, verbose=True):
     deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(INCLUDE, "mpcracing.h")]
     if not force and not _stale(PRODUCT_LIB, deps):
         return PRODUCT_LIB
-    cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
+    # -ffp-contract=off: with FMA contraction the ROCm 7.2 gfx950 build of the solver diverges from
+    # the host build on ~1/3 of the C4 fp64 instances (huge defects at iteration 0, not reproducible on
+    # any host build incl. clang -O3 -ffp-contract=fast, ASan/UBSan/MSan clean); without contraction
+    # the GPU reproduces the host build's iterates exactly (DESIGN.md §Known issues).
+    cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17", "-fPIC", "-shared",
+           "-Wno-unused-result",
            "-o", PRODUCT_LIB, os.path.join(CSRC, "mpcracing.hip")]
     if verbose:
         print(" ".join(cmd), flush=True)

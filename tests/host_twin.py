@@ -44,7 +44,7 @@ def _p(a):
     return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
 
 
-def solve(cfg, batch, tyres=None, nthreads=8):
+def solve(cfg, batch, tyres=None, nthreads=8, trace_instance=-1, trace_cap=0):
     """batch: dict of numpy arrays in ABI layout (see include/mpcracing.h)."""
     N = cfg.N
     B = batch["s0"].shape[0]
@@ -54,7 +54,10 @@ def solve(cfg, batch, tyres=None, nthreads=8):
     out = {"X": np.zeros((6, N + 1, B)), "U": np.zeros((2, N, B)), "S": np.zeros((N + 1, B)),
            "eC": np.zeros((N, B)), "eL": np.zeros((N, B)), "status": np.zeros(B, np.int32),
            "iters": np.zeros(B, np.int32), "obj": np.zeros(B), "kkt": np.zeros(B)}
-    o = abi.MROutputs(*[_p(out[k]) for k in ("X", "U", "S", "eC", "eL", "status", "iters", "obj", "kkt")])
+    if trace_cap:
+        out["trace"] = np.zeros((trace_cap, 8))
+    o = abi.MROutputs(*[_p(out.get(k)) for k in ("X", "U", "S", "eC", "eL", "status", "iters", "obj", "kkt",
+                                                 "trace")], trace_instance, trace_cap)
     if tyres is not None:
         (af, Fzf), (ar, Fzr) = tyres
         af = np.asarray(af, np.float64)

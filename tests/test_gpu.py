@@ -141,7 +141,7 @@ def test_fp32_vs_fp64_same_instances():
     s64 = BatchSolver(40, "blend", "fp64", max_batch=256)
     s32 = BatchSolver(40, "blend", "fp32", max_batch=256)
     o64, o32 = _np(s64.solve(b)), _np(s32.solve(b))
-    ok = (o64["status"] == 0) & (o32["status"] <= 1)
+    ok = (o64["status"] <= 1) & (o32["status"] <= 1)
     assert ok.mean() > 0.9
     dU = np.abs(o64["U"] - o32["U"])[:, :-1, ok]
     assert np.median(dU) < 1e-3 and np.quantile(dU, 0.99) < 5e-2
@@ -173,3 +173,54 @@ def test_abi_errors():
         s.solve(wl.make_batch("C2", limit=4))  # B > max_batch
     with pytest.raises(RuntimeError):
         BatchSolver(20, "blend_pacejka", max_batch=1).solve(wl.make_batch("C2", limit=1))  # no tyres set
+
+
+@pytest.mark.parametrize("model", ["kin", "dyn", "blend", "blend_pacejka", "dyn_pacejka"])
+def test_device_dynamics_match_host(model):
+    """The generated dynamics compiled for gfx950 vs the same source on the host (fp64)."""
+    import ctypes
+    import host_twin as ht
+    tyres = wl.tyre_coeffs("pacejka-2") if "pacejka" in model else None
+    s = BatchSolver(20, model, "fp64", max_batch=1, tyres=tyres)
+    rng = np.random.default_rng(3)
+    n = 512
+    x = np.stack([rng.normal(0, 50, n), rng.normal(0, 50, n), rng.uniform(-3, 3, n), rng.uniform(0.5, 45, n),
+                  rng.normal(0, 1, n), rng.normal(0, 0.5, n)], 1)
+    u = np.stack([rng.uniform(-1, 0.85, n), rng.uniform(-0.9, 0.9, n)], 1)
+    nu = rng.normal(0, 10, (n, 6))
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    X, Uu, NU = d(x), d(u), d(nu)
+    f, J, H = (torch.zeros((n, m), dtype=torch.float64, device="cuda") for m in (6, 48, 36))
+    rc = s.lib.mr_eval_dynamics(s.h, n, *[ctypes.c_void_p(t.data_ptr()) for t in (X, Uu, NU, f, J, H)],
+                                ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert rc == 0
+    torch.cuda.synchronize()
+    f2 = torch.zeros((n, 6), dtype=torch.float64, device="cuda")
+    rc = s.lib.mr_eval_dynamics(s.h, n, ctypes.c_void_p(X.data_ptr()), ctypes.c_void_p(Uu.data_ptr()), None,
+                                ctypes.c_void_p(f2.data_ptr()), None, None,
+                                ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert rc == 0
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(f2.cpu().numpy(), f.cpu().numpy(), rtol=1e-13, atol=1e-12)  # value-only == fjh
+    c = ht.config(20, model)
+    P = lambda a: np.ascontiguousarray(a).ctypes.data_as(ctypes.POINTER(ctypes.c_double))  # noqa: E731
+    for i in range(n):
+        fo, Jo, Ho = np.zeros(6), np.zeros(48), np.zeros(36)
+        ht.lib().mrh_eval_dynamics(ctypes.byref(c), P(tyres[0][0]) if tyres else None, tyres[0][1] if tyres else 0.0,
+                                   P(tyres[1][0]) if tyres else None, tyres[1][1] if tyres else 0.0,
+                                   P(x[i]), P(u[i]), P(nu[i]), P(fo), P(Jo), P(Ho))
+        np.testing.assert_allclose(f[i].cpu().numpy(), fo, rtol=1e-13, atol=1e-12)
+        np.testing.assert_allclose(J[i].cpu().numpy(), Jo, rtol=1e-11, atol=1e-11)
+        np.testing.assert_allclose(H[i].cpu().numpy(), Ho, rtol=1e-9, atol=1e-9 * max(1, np.abs(Ho).max()))
+
+
+def test_c4_fp64_gpu_vs_host_statuses():
+    import host_twin as ht
+    b = wl.make_batch("C4", limit=64)
+    s = BatchSolver(40, "blend", "fp64", max_batch=64, acceptable_iter=0)
+    o = _np(s.solve(b))
+    h = ht.solve(ht.config(40, "blend", "fp64", tol=1e-8), b, nthreads=16)
+    print("gpu status", o["status"].tolist(), "iters", o["iters"].tolist())
+    print("host status", h["status"].tolist(), "iters", h["iters"].tolist())
+    print("gpu kkt", o["kkt"].tolist())
+    assert (o["status"] == h["status"]).all()
