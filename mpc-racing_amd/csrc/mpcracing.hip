@@ -1,16 +1,14 @@
 // libmpcracing.so -- gfx950 batched racing-MPC solver and its C ABI (include/mpcracing.h).
 //
-// One thread per MPC instance runs the whole interior-point solve (mr_solver.h);
-// the per-stage working set lives in an HBM workspace in structure-of-arrays layout
-// [stage][field][instance] so every load/store of a wavefront is one coalesced
-// 64 x sizeof(T) segment.  Instances are independent, so there is no inter-thread
-// communication and a launch needs no synchronisation besides its end.
+// One 64-lane wavefront per MPC instance runs the interior-point solve (mr_wave.h):
+// lanes = stages for the stage-parallel sweeps, lanes = matrix rows for the Riccati
+// recursion.  Instances are independent: no inter-workgroup communication.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <string.h>
 #include <string>
 
-#include "mr_batch.h"
+#include "mr_wave.h"
 
 using namespace mr;
 
@@ -18,7 +16,6 @@ struct mr_handle {
   mr_config cfg;
   void* ws;
   size_t ws_bytes;
-  int64_t ws_stride;
   TyreCoef<double> tf, tr;
   int have_tyres;
 };
@@ -36,31 +33,28 @@ static int fail(int code, const std::string& msg) {
     if (e_ != hipSuccess) return fail(MR_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
   } while (0)
 
-constexpr int kBlock = 64;
-
+// One 64-lane workgroup (= one wavefront) per instance: lanes are stages / matrix rows
+// of that instance (mr_wave.h); the grid is the batch.
+#ifndef MR_WAVES_PER_SIMD
+#define MR_WAVES_PER_SIMD 2
+#endif
 template <typename T, int MODEL>
-__global__ __launch_bounds__(kBlock) void mr_solve_kernel(ProbParams<T> P, mr_inputs in, mr_outputs out, int B,
-                                                          T* ws, int64_t stride) {
-  const int i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= B) return;
-  WS<T> W{ws + i, stride};
-  solve_instance<T, MODEL>(P, in, out, B, i, W);
+__global__ __launch_bounds__(WL, MR_WAVES_PER_SIMD) void mr_wave_kernel(ProbParams<T> P, mr_inputs in, mr_outputs out, int B, T* ws) {
+  __shared__ T lds[LDS_WORDS];
+  const int i = blockIdx.x;
+  Wv w{(int)threadIdx.x};
+  solve_instance_wave<T, MODEL>(P, in, out, B, i, ws + (int64_t)i * WS_WORDS, lds, w);
 }
 
-template <typename T>
-static size_t elem_size() { return sizeof(T); }
-
 static size_t ws_bytes_per_instance(const mr_config& c) {
-  const size_t per = (size_t)WF::NF * (size_t)(c.N + 1);
-  return per * (c.precision == MR_PREC_FP32 ? sizeof(float) : sizeof(double));
+  return (size_t)WS_WORDS * (c.precision == MR_PREC_FP32 ? sizeof(float) : sizeof(double));
 }
 
 template <typename T, int MODEL>
 static int launch(mr_handle* h, int B, const mr_inputs* in, mr_outputs* out, hipStream_t st) {
   ProbParams<T> P;
   fill_params<T>(h->cfg, h->tf, h->tr, P);
-  dim3 grid((B + kBlock - 1) / kBlock), block(kBlock);
-  hipLaunchKernelGGL((mr_solve_kernel<T, MODEL>), grid, block, 0, st, P, *in, *out, B, (T*)h->ws, h->ws_stride);
+  hipLaunchKernelGGL((mr_wave_kernel<T, MODEL>), dim3(B), dim3(WL), 0, st, P, *in, *out, B, (T*)h->ws);
   HIP_TRY(hipGetLastError());
   return MR_OK;
 }
@@ -121,7 +115,7 @@ int mr_config_default(mr_config* cfg) {
 
 int mr_create(mr_handle** out, const mr_config* cfg) {
   if (!out || !cfg) return fail(MR_ERR_ARG, "null argument");
-  if (cfg->N < 1 || cfg->N > 1000) return fail(MR_ERR_ARG, "N out of range");
+  if (cfg->N < 1 || cfg->N > WL - 1) return fail(MR_ERR_ARG, "N out of range (1..63: one wavefront lane per stage)");
   if (cfg->model < 0 || cfg->model > 4) return fail(MR_ERR_ARG, "unknown model");
   if (cfg->precision != MR_PREC_FP64 && cfg->precision != MR_PREC_FP32) return fail(MR_ERR_ARG, "bad precision");
   if (cfg->max_batch < 1) return fail(MR_ERR_ARG, "max_batch < 1");
@@ -132,7 +126,6 @@ int mr_create(mr_handle** out, const mr_config* cfg) {
   h->have_tyres = 0;
   memset(&h->tf, 0, sizeof(h->tf));
   memset(&h->tr, 0, sizeof(h->tr));
-  h->ws_stride = cfg->max_batch;
   h->ws_bytes = ws_bytes_per_instance(*cfg) * (size_t)cfg->max_batch;
   hipError_t e = hipMalloc(&h->ws, h->ws_bytes);
   if (e != hipSuccess) {

@@ -1,28 +1,49 @@
 // Host (g++) build of the solver core -- TEST HARNESS ONLY.
 //
 // libmpcracing_host.so runs the very same per-instance solver source as the
-// gfx950 kernels, on CPU threads, so that the solver logic can be checked
+// gfx950 kernel (mr_wave.h), each instance as an emulated 64-lane wavefront, so that the solver logic can be checked
 // against the oracle in the CPU test suite (no GPU in the build container).
 // The product path (mpc-racing_amd/control/MPC.py, mpcracing.batch) never
 // loads this library; it requires libmpcracing.so and a GPU.
 #include <stdlib.h>
 #include <string.h>
 #include <vector>
-#include "mr_batch.h"
+#include "mr_wave.h"
 
 using namespace mr;
 
+template <typename T, int MODEL>
+struct Job {
+  const ProbParams<T>* P;
+  const mr_inputs* in;
+  const mr_outputs* out;
+  int64_t B, i;
+  T* ws;
+  T* lds;
+};
+
+template <typename T, int MODEL>
+static void wave_body(HostWave* hw, int lane, void* arg) {
+  Job<T, MODEL>* j = (Job<T, MODEL>*)arg;
+  Wv w{lane, hw};
+  solve_instance_wave<T, MODEL>(*j->P, *j->in, *j->out, j->B, j->i, j->ws, j->lds, w);
+  wsync(w);  // final rendezvous: every lane done before the wave is torn down
+}
+
+// Each instance runs as one emulated wavefront (64 fibers, mr_wave_prims.h) on one CPU thread.
 template <typename T, int MODEL>
 static void run(const mr_config& c, const TyreCoef<double>& tf, const TyreCoef<double>& tr, int B,
                 const mr_inputs& in, const mr_outputs& out, int nthreads) {
   ProbParams<T> P;
   fill_params<T>(c, tf, tr, P);
-  // poisoned workspace: any read-before-write shows up as NaN (hipMalloc memory is not zeroed)
-  std::vector<T> ws((size_t)WF::NF * (c.N + 1) * (size_t)B, (T)NAN);
 #pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
   for (int i = 0; i < B; ++i) {
-    WS<T> W{ws.data() + i, (int64_t)B};
-    solve_instance<T, MODEL>(P, in, out, B, i, W);
+    // poisoned workspace / LDS: any read-before-write shows up as NaN (device memory is not zeroed)
+    std::vector<T> ws((size_t)WS_WORDS, (T)NAN), lds((size_t)LDS_WORDS, (T)NAN);
+    Job<T, MODEL> job{&P, &in, &out, (int64_t)B, (int64_t)i, ws.data(), lds.data()};
+    HostWave* hw = new HostWave();
+    host_wave_run(*hw, &wave_body<T, MODEL>, &job);
+    delete hw;
   }
 }
 

@@ -1,0 +1,864 @@
+// Wave-per-instance interior-point solver of the racing-MPC NLP (the gfx950 product kernel).
+//
+// Replaces the CasADi Opti + IPOPT solve of control/MPC.py:30-181.  Same NLP, same
+// stage-wise restatement and the same IPOPT-rule algorithm as the stage-level pieces in
+// mr_solver.h (formulation notes there), but one 64-lane wavefront cooperates on one
+// instance instead of one lane running it alone:
+//
+//   * lanes = stages (k = lane <= N <= 63) for every stage-parallel sweep: evaluation of
+//     dynamics/derivatives/cost/rows, slack and multiplier steps, line-search trial points;
+//     KKT-error and merit terms are butterfly reductions over the wave;
+//   * lanes = matrix rows for the backward Riccati recursion (sequential in k): lane r owns
+//     row r of the 11x11 cost-to-go P and of the 14x14 stage Q-function; the two dense
+//     products P*[A B] and [A B]^T*(P*[A B]) exchange rows through ~3 KB of LDS;
+//   * the forward substitution (sequential, 11+3 values) runs wave-uniform.
+//
+// Working set per instance (global workspace, base + i * WS_WORDS):
+//   ss[f][64]   per-stage iterate / step fields, lane-contiguous (coalesced per field)
+//   rc[k][336]  per-stage Riccati record (stage Hessian, Jacobian, gradients, P, K)
+#pragma once
+#include "mr_batch.h"
+#include "mr_wave_prims.h"
+
+// The sweeps are separate (non-inlined) device functions so each gets its own register
+// allocation; only the small wave-uniform iteration state is live across the calls.
+#if MR_DEVICE_BUILD
+#define MR_SWEEP __device__ __attribute__((noinline))
+#else
+#define MR_SWEEP inline
+#endif
+
+namespace mr {
+
+struct SSF {
+  enum {
+    Z0 = 0, Z1 = Z0 + NZS, DZ = Z1 + NZS, S0 = DZ + NZS, S1 = S0 + NI, LAM = S1 + NI, DLAM = LAM + NI,
+    DS = DLAM + NI, NU = DS + NI, DNU = NU + NX, NF = DNU + NX
+  };
+};
+struct RCF {
+  enum {
+    H = 0, G0 = H + NH, G1 = G0 + NZ, GL = G1 + NZ, J = GL + NZ, C = J + 48, P = C + NX, PV0 = P + NP,
+    PV1 = PV0 + NX, K = PV1 + NX, K0 = K + NU * NX, K1 = K0 + NU, NF = K1 + NU
+  };
+};
+constexpr int RC_STRIDE = 336;
+static_assert(RCF::NF <= RC_STRIDE, "record");
+constexpr int64_t WS_WORDS = (int64_t)SSF::NF * WL + (int64_t)RC_STRIDE * WL;
+constexpr int LX_OFF = 0, LQ_OFF = 11 * 16, LW_OFF = LQ_OFF + 16 * 16, LP_OFF = LW_OFF + 11 * 4;
+constexpr int LDS_WORDS = LP_OFF + 11 * 12;
+
+// lower-triangular solves with L packed (00,10,11,20,21,22) as produced by chol3
+template <typename T>
+MR_HD void lsolve3(const T* L, T* b) {
+  b[0] = b[0] / L[0];
+  b[1] = (b[1] - L[1] * b[0]) / L[2];
+  b[2] = (b[2] - L[3] * b[0] - L[4] * b[1]) / L[5];
+}
+template <typename T>
+MR_HD void ltsolve3(const T* L, T* b) {
+  b[2] = b[2] / L[5];
+  b[1] = (b[1] - L[4] * b[2]) / L[2];
+  b[0] = (b[0] - L[1] * b[1] - L[3] * b[2]) / L[0];
+}
+
+// Inequality rows of stage k (MPC.py:134-149) with their fixed sparsity, so every index is a
+// compile-time constant after unrolling (no private-memory arrays):
+//   r = 0 thr box, 1 steer box, 2 dS box, 3/4 rate rows vs p (or state0 at k = 0),
+//   5/6 wrap-around rate rows U[:,0] - U[:,N-1] at k = N-1 via the frozen copy w.
+//   c_r(z) = sum_a RS(a) z[RI(r, a)],  lo_r <= c_r <= hi_r.
+MR_HD constexpr int RN(int r) { return r < 3 ? 1 : 2; }
+MR_HD constexpr int RI(int r, int a) {
+  return r == 0 ? 11 : r == 1 ? 12 : r == 2 ? 13 : r == 3 ? (a ? 7 : 11) : r == 4 ? (a ? 8 : 12) : r == 5 ? (a ? 11 : 9)
+                                                                                                         : (a ? 12 : 10);
+}
+MR_HD constexpr int RS(int a) { return a ? -1 : 1; }
+
+template <typename T>
+MR_HD void row_bounds(const ProbParams<T>& P, const Inst<T>& I, int k, int r, int& act, T& lo, T& hi) {
+  const int N = P.N;
+  act = 0; lo = T(0); hi = T(0);
+  if (k == N) return;
+  if (r == 0) { act = 1; lo = P.min_thr; hi = I.d_max; }          // MPC.py:138-139 (class-attribute d_max)
+  else if (r == 1) { act = 1; lo = P.min_steer; hi = P.max_steer; }  // :140-141
+  else if (r == 2) { act = 1; lo = P.min_ds; hi = P.Ts * P.v_max; }  // :134
+  else if (r == 3) { act = (k >= 1 || I.has_thr0) ? 1 : 0; lo = P.min_dthr; hi = P.max_dthr; }      // :142 / :145-146
+  else if (r == 4) { act = (k >= 1 || I.has_steer0) ? 1 : 0; lo = P.min_dsteer; hi = P.max_dsteer; }  // :143 / :148-149
+  else if (r == 5) { act = (k == N - 1 && N >= 2) ? 1 : 0; lo = P.min_dthr; hi = P.max_dthr; }       // :142 at i = 0
+  else { act = (k == N - 1 && N >= 2) ? 1 : 0; lo = P.min_dsteer; hi = P.max_dsteer; }                // :143 at i = 0
+}
+template <typename T>
+MR_HD T row_c(int r, const T* z) { return RN(r) == 1 ? z[RI(r, 0)] : z[RI(r, 0)] - z[RI(r, 1)]; }
+
+template <typename T, int MODEL>
+struct WaveSolver {
+  const ProbParams<T>& P;
+  const Inst<T>& I;
+  Wv w;
+  T* ss;
+  T* rc;
+  T* lds;
+  int N, ln;
+  // wave-uniform iteration state
+  int cur;
+  T mu, sc, delta_last;
+  T alpha_p, alpha_d;
+  T theta_max, theta_min;
+  T filt_th[FMAX], filt_ph[FMAX];
+  int nfilt;
+  T stat_max, pr_max, theta, slam_max, slam_min, nu1, lam1, fval, logs;
+  int me, mi;
+  double* trace = nullptr;
+  int trace_cap = 0;
+
+  MR_HD WaveSolver(const ProbParams<T>& P_, const Inst<T>& I_, Wv w_, T* ws, T* lds_)
+      : P(P_), I(I_), w(w_), ss(ws), rc(ws + (int64_t)SSF::NF * WL), lds(lds_), N(P_.N), ln(w_.lane) {}
+
+  MR_HD T& S(int f) const { return ss[f * WL + ln]; }
+  MR_HD T* R(int k) const { return rc + (int64_t)k * RC_STRIDE; }
+  MR_HD bool own() const { return ln <= N; }
+  MR_HD int zf(int b) const { return b ? SSF::Z1 : SSF::Z0; }
+  MR_HD int sf(int b) const { return b ? SSF::S1 : SSF::S0; }
+  MR_HD int nxt() const { return (ln + 1) & (WL - 1); }
+
+  MR_HD void load_z(int b, T* z) const {
+    for (int i = 0; i < NZS; ++i) z[i] = own() ? S(zf(b) + i) : T(0);
+    if (ln >= N) { z[11] = T(0); z[12] = T(0); z[13] = T(0); }
+  }
+
+  MR_HD void row_values(int k, const T* z, const Err<T>& e, T* d, int* act) const {
+#pragma unroll
+    for (int r = 0; r < NROW; ++r) {
+      int a;
+      T lo, hi;
+      row_bounds(P, I, k, r, a, lo, hi);
+      const T c = row_c(r, z);
+      act[2 * r] = act[2 * r + 1] = a;
+      d[2 * r] = c - lo;
+      d[2 * r + 1] = hi - c;
+    }
+    const int la = lane_active(P, k) ? 1 : 0;
+    act[JL] = act[JL + 1] = act[JL + 2] = la;
+    lane_d(I, e.eC, z[14], d + JL);
+  }
+
+  MR_HD void lane_block(int b, const T* d, T& htt, T& hd, T& gt0, T& gt1) const {
+    htt = T(0); gt0 = sc * P.lane_pen; gt1 = T(0);
+    T sig[3];
+    for (int q = 0; q < 3; ++q) {
+      T s = S(sf(b) + JL + q), lam = S(SSF::LAM + JL + q);
+      sig[q] = lam / s;
+      htt += sig[q];
+      gt0 += sig[q] * (d[JL + q] - s);
+      gt1 -= T(1) / s;
+    }
+    hd = sig[0] - sig[1];
+  }
+
+  // ---------------- initialisation (MPC.py:100-131) ----------------
+  MR_SWEEP void init(const double* u_init, int64_t ustride) {
+    cur = 0;
+    T z[NZS], zn[NX], my[NZS];
+    for (int i = 0; i < NZS; ++i) { z[i] = T(0); my[i] = T(0); }
+    for (int i = 0; i < 6; ++i) z[i] = I.x0[i];
+    z[7] = I.has_thr0 ? I.thr0 : T(0);
+    z[8] = I.has_steer0 ? I.steer0 : T(0);
+    // initial-guess rollout (sequential, wave-uniform); lane k keeps stage k
+    for (int k = 0; k <= N; ++k) {
+      if (k < N) {
+        if (u_init) { z[11] = T(u_init[(int64_t)k * ustride]); z[12] = T(u_init[(int64_t)(N + k) * ustride]); }
+        else { z[11] = I.thr0; z[12] = I.steer0; }
+        z[13] = P.Ts * P.v_max;  // S_i = s0 + i*Ts*v_max (MPC.py:127)
+      } else {
+        z[11] = z[12] = z[13] = T(0);
+      }
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      z[14] = lane_active(P, k) ? mr_max(mr_abs(e.eC) - I.max_err, T(0)) + T(1e-2) : T(0);
+      if (ln == k)
+        for (int i = 0; i < NZS; ++i) my[i] = z[i];
+      if (k < N) {
+        faug<T, MODEL>(P, k, z, zn);
+        for (int i = 0; i < NX; ++i) z[i] = zn[i];
+      }
+    }
+    T gmax = T(0), th = T(0);
+    if (own()) {
+      const int k = ln;
+      for (int i = 0; i < NZS; ++i) S(SSF::Z0 + i) = my[i];
+      Err<T> e;
+      errors(I, my[0], my[1], my[6], e, false);
+      T g[NZ];
+      for (int i = 0; i < NZ; ++i) g[i] = T(0);
+      stage_cost(P, I, k, my, e, T(1), g, (T*)nullptr);
+      for (int i = 0; i < NZ; ++i) gmax = mr_max(gmax, mr_abs(g[i]));
+      T d[NI];
+      int act[NI];
+      row_values(k, my, e, d, act);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        T push;
+        if (j < JL) {
+          int ra;
+          T lo, hi;
+          row_bounds(P, I, k, j / 2, ra, lo, hi);
+          T bnd = (j & 1) ? mr_abs(hi) : mr_abs(lo);
+          push = mr_min(T(1e-2) * mr_max(T(1), bnd), T(1e-2) * (hi - lo));
+        } else {
+          push = j < JL + 2 ? T(1e-2) * mr_max(T(1), I.max_err) : T(1e-2);
+        }
+        T s = act[j] ? mr_max(d[j], push) : T(1);
+        S(SSF::S0 + j) = s;
+        S(SSF::LAM + j) = act[j] ? T(1) : T(0);
+        S(SSF::DLAM + j) = T(0);
+        if (act[j]) th += mr_abs(d[j] - s);
+      }
+      for (int i = 0; i < NX; ++i) { S(SSF::NU + i) = T(0); S(SSF::DNU + i) = T(0); }
+    }
+    gmax = wmax(w, gmax);
+    th = wsum(w, th);
+    sc = gmax > T(0) ? mr_min(T(1), T(100) / gmax) : T(1);
+    mu = T(0.1);
+    delta_last = T(0);
+    alpha_p = alpha_d = T(0);
+    theta_max = T(1e4) * mr_max(T(1), th);
+    theta_min = T(1e-4) * mr_max(T(1), th);
+    nfilt = 0;
+  }
+
+  // ---------------- sweep 1: evaluation, KKT error terms, stage QP data (lane = stage) ----------------
+  MR_SWEEP void eval_sweep(T mu_prev) {
+    const T kappa_sigma = T(1e10);
+    const int k = ln;
+    T st_l = T(0), pr_l = T(0), th_l = T(0), smax_l = T(0), smin_l = T(1e30), nu1_l = T(0), lam1_l = T(0),
+      f_l = T(0), lg_l = T(0);
+    int mi_l = 0;
+    // lazy multiplier update nu_k += alpha_p * dnu_k (stages 1..N)
+    T nuk[NX];
+    for (int i = 0; i < NX; ++i) nuk[i] = T(0);
+    if (own() && k >= 1) {
+      for (int i = 0; i < NX; ++i) {
+        T v = S(SSF::NU + i) + alpha_p * S(SSF::DNU + i);
+        S(SSF::NU + i) = v;
+        nuk[i] = v;
+        nu1_l += mr_abs(v);
+      }
+    }
+    T z[NZS];
+    load_z(cur, z);
+    T nun[NX], znext[NX];
+    for (int i = 0; i < NX; ++i) {
+      nun[i] = wshfl(w, nuk[i], nxt());
+      znext[i] = wshfl(w, z[i], nxt());
+    }
+    if (own()) {
+      T* Rk = R(k);
+      T H[NH], g0[NZ], g1[NZ], gl[NZ], st[NZ];
+      for (int i = 0; i < NH; ++i) H[i] = T(0);
+      for (int i = 0; i < NZ; ++i) { g0[i] = g1[i] = gl[i] = st[i] = T(0); }
+      if (k < N) {
+        T Hd[36], J[48], fx[6];
+        Dyn<T, MODEL>::fjh(P, z, z + NX, nun, fx, J, Hd);
+        const int map[8] = {0, 1, 2, 3, 4, 5, 11, 12};
+        int q = 0;
+        for (int a = 0; a < 8; ++a)
+          for (int bb = a; bb < 8; ++bb, ++q) H[hidx(map[a], map[bb])] += Hd[q];
+        T c[NX];
+        for (int i = 0; i < 6; ++i) c[i] = fx[i] - znext[i];
+        c[6] = z[6] + z[13] - znext[6];
+        c[7] = z[11] - znext[7];
+        c[8] = z[12] - znext[8];
+        c[9] = (k == 0 ? z[11] : z[9]) - znext[9];
+        c[10] = (k == 0 ? z[12] : z[10]) - znext[10];
+        for (int i = 0; i < NX; ++i) {
+          Rk[RCF::C + i] = c[i];
+          pr_l = mr_max(pr_l, mr_abs(c[i]));
+          th_l += mr_abs(c[i]);
+        }
+        for (int i = 0; i < 48; ++i) Rk[RCF::J + i] = J[i];
+        T at[NX], bt[NU];
+        apply_At(J, k, nun, at);
+        apply_Bt(J, k, nun, bt);
+        for (int i = 0; i < NX; ++i) st[i] += at[i];
+        for (int i = 0; i < NU; ++i) st[NX + i] += bt[i];
+      }
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, true);
+      f_l += stage_cost(P, I, k, z, e, sc, gl, H);
+      for (int i = 0; i < NZ; ++i) { g0[i] += gl[i]; st[i] += gl[i]; }
+      if (k >= 1)
+        for (int i = 0; i < NX; ++i) st[i] -= nuk[i];
+      T d[NI];
+      int act[NI];
+      row_values(k, z, e, d, act);
+      T lam_j[NI], s_j[NI];
+      for (int j = 0; j < NI; ++j) {
+        lam_j[j] = T(0);
+        s_j[j] = T(1);
+        if (!act[j]) continue;
+        T s = S(sf(cur) + j);
+        T lam = S(SSF::LAM + j) + alpha_d * S(SSF::DLAM + j);
+        lam = mr_min(mr_max(lam, mu_prev / (kappa_sigma * s)), kappa_sigma * mu_prev / s);
+        S(SSF::LAM + j) = lam;
+        lam_j[j] = lam;
+        s_j[j] = s;
+        T rd = d[j] - s;
+        pr_l = mr_max(pr_l, mr_abs(rd));
+        th_l += mr_abs(rd);
+        T sl = s * lam;
+        smax_l = mr_max(smax_l, sl);
+        smin_l = mr_min(smin_l, sl);
+        lam1_l += mr_abs(lam);
+        lg_l += mr_log(s);
+        mi_l += 1;
+      }
+#pragma unroll
+      for (int r = 0; r < NROW; ++r) {
+        if (!act[2 * r]) continue;
+        T sig_sum = T(0), gsc0 = T(0), gsc1 = T(0), lamdiff = T(0);
+#pragma unroll
+        for (int sd = 0; sd < 2; ++sd) {
+          int j = 2 * r + sd;
+          T sig = lam_j[j] / s_j[j];
+          T sgn = sd == 0 ? T(1) : T(-1);
+          sig_sum += sig;
+          gsc0 += sgn * sig * (d[j] - s_j[j]);
+          gsc1 += -sgn / s_j[j];
+          lamdiff += sgn * lam_j[j];
+        }
+#pragma unroll
+        for (int a = 0; a < RN(r); ++a) {
+          const T sa = T(RS(a));
+          g0[RI(r, a)] += sa * gsc0;
+          g1[RI(r, a)] += sa * gsc1;
+          st[RI(r, a)] -= lamdiff * sa;
+#pragma unroll
+          for (int bb = a; bb < RN(r); ++bb) H[hidx(RI(r, a), RI(r, bb))] += sig_sum * sa * T(RS(bb));
+        }
+      }
+      if (lane_active(P, k)) {
+        const int id3[3] = {0, 1, 6};
+        T s0 = s_j[JL], s1 = s_j[JL + 1];
+        T sig0 = lam_j[JL] / s0, sig1 = lam_j[JL + 1] / s1;
+        T lamdiff = lam_j[JL] - lam_j[JL + 1];
+        T gz0 = sig0 * (d[JL] - s0) - sig1 * (d[JL + 1] - s1);
+        T gz1 = -T(1) / s0 + T(1) / s1;
+        T htt, hd, gt0, gt1;
+        lane_block(cur, d, htt, hd, gt0, gt1);
+        int q = 0;
+        for (int a = 0; a < 3; ++a) {
+          g0[id3[a]] += e.gC[a] * (gz0 - hd * gt0 / htt);
+          g1[id3[a]] += e.gC[a] * (gz1 - hd * gt1 / htt);
+          st[id3[a]] -= lamdiff * e.gC[a];
+          for (int bb = a; bb < 3; ++bb, ++q)
+            H[hidx(id3[a], id3[bb])] += (sig0 + sig1 - hd * hd / htt) * e.gC[a] * e.gC[bb] - lamdiff * e.hC[q];
+        }
+        f_l += sc * P.lane_pen * z[14];
+        T stt = sc * P.lane_pen - lam_j[JL] - lam_j[JL + 1] - lam_j[JL + 2];
+        st_l = mr_max(st_l, mr_abs(stt));
+      }
+      if (k >= 1)
+        for (int i = 0; i < NX; ++i) st_l = mr_max(st_l, mr_abs(st[i]));
+      if (k < N)
+        for (int i = NX; i < NZ; ++i) st_l = mr_max(st_l, mr_abs(st[i]));
+      for (int i = 0; i < NH; ++i) Rk[RCF::H + i] = H[i];
+      for (int i = 0; i < NZ; ++i) { Rk[RCF::G0 + i] = g0[i]; Rk[RCF::G1 + i] = g1[i]; Rk[RCF::GL + i] = gl[i]; }
+    }
+    stat_max = wmax(w, st_l);
+    pr_max = wmax(w, pr_l);
+    theta = wsum(w, th_l);
+    slam_max = wmax(w, smax_l);
+    slam_min = wmin(w, smin_l);
+    nu1 = wsum(w, nu1_l);
+    lam1 = wsum(w, lam1_l);
+    fval = wsum(w, f_l);
+    logs = wsum(w, lg_l);
+    mi = wsum(w, mi_l);
+    me = NX * (N + 1);
+    wsync(w);  // stage records visible to every lane before the Riccati sweep
+  }
+
+  MR_HD T kkt_error(T m) const {
+    const T smax = T(100);
+    T sd = mr_max(smax, (nu1 + lam1) / T(me + (mi > 0 ? mi : 1))) / smax;
+    T scm = mr_max(smax, lam1 / T(mi > 0 ? mi : 1)) / smax;
+    T cerr = mr_max(mr_abs(slam_max - m), mr_abs(m - slam_min));
+    if (mi == 0) cerr = T(0);
+    return mr_max(mr_max(stat_max / sd, pr_max), cerr / scm);
+  }
+
+  // ---------------- sweep 2: Riccati factorisation (backward; lane = matrix row) ----------------
+  //   X = [P' E | P' c + p0' | p1']          (11 x 16, row r on lane r)
+  //   Q = H + E^T X (+ delta I), q0 | q1     (14 x 16, row a on lane a)
+  //   W = L^{-1} Q_ux with L L^T = Q_uu;  P = Q_xx - W^T W;  K = -L^{-T} W
+  MR_SWEEP bool riccati(T delta) {
+    const int r = ln;
+    T* LX = lds + LX_OFF;
+    T* LQ = lds + LQ_OFF;
+    T* LW = lds + LW_OFF;
+    T* LP = lds + LP_OFF;
+    T Prow[NX], p0r = T(0), p1r = T(0);
+    for (int j = 0; j < NX; ++j) Prow[j] = T(0);
+    if (r < NX) {
+      T* Rn = R(N);
+      for (int j = 0; j < NX; ++j) Prow[j] = Rn[RCF::H + hidx(r, j)] + (r == j ? delta : T(0));
+      p0r = Rn[RCF::G0 + r];
+      p1r = Rn[RCF::G1 + r];
+      for (int j = r; j < NX; ++j) Rn[RCF::P + pidx(r, j)] = Prow[j];
+      Rn[RCF::PV0 + r] = p0r;
+      Rn[RCF::PV1 + r] = p1r;
+    }
+    for (int k = N - 1; k >= 0; --k) {
+      T* Rk = R(k);
+      // R1: row r of X (uniform J, c)
+      if (r < NX) {
+        T J[48], c[NX];
+        for (int i = 0; i < 48; ++i) J[i] = Rk[RCF::J + i];
+        for (int i = 0; i < NX; ++i) c[i] = Rk[RCF::C + i];
+        T xr[16];
+        for (int j = 0; j < 6; ++j) {
+          T acc = T(0);
+          for (int l = 0; l < 6; ++l) acc += Prow[l] * J[l * 8 + j];
+          xr[j] = acc;
+        }
+        T a0 = T(0), a1 = T(0);
+        for (int l = 0; l < 6; ++l) { a0 += Prow[l] * J[l * 8 + 6]; a1 += Prow[l] * J[l * 8 + 7]; }
+        xr[6] = Prow[6];
+        xr[7] = T(0);
+        xr[8] = T(0);
+        xr[9] = k > 0 ? Prow[9] : T(0);
+        xr[10] = k > 0 ? Prow[10] : T(0);
+        xr[11] = a0 + Prow[7] + (k == 0 ? Prow[9] : T(0));
+        xr[12] = a1 + Prow[8] + (k == 0 ? Prow[10] : T(0));
+        xr[13] = Prow[6];
+        T v = p0r;
+        for (int l = 0; l < NX; ++l) v += Prow[l] * c[l];
+        xr[14] = v;
+        xr[15] = p1r;
+        for (int j = 0; j < 16; ++j) LX[r * 16 + j] = xr[j];
+      }
+      wsync(w);
+      // R2: row a of Q = H_k + e_a^T X, e_a = column a of E = [A B]
+      T qa[16];
+      for (int b = 0; b < 16; ++b) qa[b] = T(0);
+      if (r < NZ) {
+        const int a = r;
+        const int ja = a < 6 ? a : (a == 11 ? 6 : (a == 12 ? 7 : -1));
+        T e[NX];
+        for (int i = 0; i < 6; ++i) e[i] = ja >= 0 ? Rk[RCF::J + i * 8 + ja] : T(0);
+        e[6] = (a == 6 || a == 13) ? T(1) : T(0);
+        e[7] = a == 11 ? T(1) : T(0);
+        e[8] = a == 12 ? T(1) : T(0);
+        e[9] = (k > 0 ? a == 9 : a == 11) ? T(1) : T(0);
+        e[10] = (k > 0 ? a == 10 : a == 12) ? T(1) : T(0);
+        for (int b = 0; b < 16; ++b) {
+          T acc = T(0);
+          for (int i = 0; i < NX; ++i) acc += e[i] * LX[i * 16 + b];
+          qa[b] = acc;
+        }
+        for (int b = 0; b < NZ; ++b) qa[b] += Rk[RCF::H + hidx(a, b)] + (a == b ? delta : T(0));
+        qa[14] += Rk[RCF::G0 + a];
+        qa[15] += Rk[RCF::G1 + a];
+        for (int b = 0; b < 16; ++b) LQ[a * 16 + b] = qa[b];
+      }
+      wsync(w);
+      // R3: Q_uu = L L^T (wave-uniform), W column r, new P row r
+      T Rh[6] = {LQ[11 * 16 + 11], LQ[11 * 16 + 12], LQ[11 * 16 + 13],
+                 LQ[12 * 16 + 12], LQ[12 * 16 + 13], LQ[13 * 16 + 13]};
+      T L[6];
+      if (!chol3(Rh, L)) return false;  // uniform: identical inputs and code on every lane
+      T w0[3] = {LQ[11 * 16 + 14], LQ[12 * 16 + 14], LQ[13 * 16 + 14]};
+      T w1[3] = {LQ[11 * 16 + 15], LQ[12 * 16 + 15], LQ[13 * 16 + 15]};
+      lsolve3(L, w0);
+      lsolve3(L, w1);
+      T Wr[3] = {qa[11], qa[12], qa[13]};  // Q_ux[:, r] = Q_xu[r, :] (row r, symmetric)
+      lsolve3(L, Wr);
+      if (r < NX)
+        for (int m = 0; m < 3; ++m) LW[r * 4 + m] = Wr[m];
+      wsync(w);
+      T Pn[NX];
+      for (int j = 0; j < NX; ++j) Pn[j] = T(0);
+      if (r < NX) {
+        for (int j = 0; j < NX; ++j)
+          Pn[j] = qa[j] - (Wr[0] * LW[j * 4 + 0] + Wr[1] * LW[j * 4 + 1] + Wr[2] * LW[j * 4 + 2]);
+        T p0n = qa[14] - (Wr[0] * w0[0] + Wr[1] * w0[1] + Wr[2] * w0[2]);
+        T p1n = qa[15] - (Wr[0] * w1[0] + Wr[1] * w1[1] + Wr[2] * w1[2]);
+        T kr[3] = {Wr[0], Wr[1], Wr[2]};
+        ltsolve3(L, kr);
+        for (int j = r; j < NX; ++j) {
+          Rk[RCF::P + pidx(r, j)] = Pn[j];
+          LP[r * 12 + j] = Pn[j];
+        }
+        Rk[RCF::PV0 + r] = p0n;
+        Rk[RCF::PV1 + r] = p1n;
+        for (int a = 0; a < NU; ++a) Rk[RCF::K + a * NX + r] = -kr[a];
+        if (r == 0) {
+          T k0[3] = {w0[0], w0[1], w0[2]}, k1[3] = {w1[0], w1[1], w1[2]};
+          ltsolve3(L, k0);
+          ltsolve3(L, k1);
+          for (int a = 0; a < NU; ++a) { Rk[RCF::K0 + a] = -k0[a]; Rk[RCF::K1 + a] = -k1[a]; }
+        }
+        p0r = p0n;
+        p1r = p1n;
+      }
+      wsync(w);
+      // symmetric P for the next stage: upper triangle from the owning rows
+      if (r < NX)
+        for (int j = 0; j < NX; ++j) Prow[j] = j >= r ? Pn[j] : LP[j * 12 + r];
+    }
+    wsync(w);  // records (P, K) visible to every lane
+    return true;
+  }
+
+  // ---------------- sweep 3: forward substitution, slack/dual steps ----------------
+  MR_SWEEP void forward(T& ap, T& ad, T& gphi) {
+    const T tau = mr_max(T(0.99), T(1) - mu);
+    T dx[NX], dz[NZS];
+    for (int i = 0; i < NX; ++i) dx[i] = T(0);
+    for (int i = 0; i < NZS; ++i) dz[i] = T(0);
+    // sequential part: dz_k = (dx_k, K_k dx_k + k0 + mu k1), dx_{k+1} = A dx + B du + c (wave-uniform)
+    for (int k = 0; k < N; ++k) {
+      const T* Rk = R(k);
+      T du[NU];
+      for (int a = 0; a < NU; ++a) {
+        T v = Rk[RCF::K0 + a] + mu * Rk[RCF::K1 + a];
+        for (int j = 0; j < NX; ++j) v += Rk[RCF::K + a * NX + j] * dx[j];
+        du[a] = v;
+      }
+      if (ln == k) {
+        for (int i = 0; i < NX; ++i) dz[i] = dx[i];
+        for (int a = 0; a < NU; ++a) dz[NX + a] = du[a];
+      }
+      T J[48], c[NX], xn[NX];
+      for (int i = 0; i < 48; ++i) J[i] = Rk[RCF::J + i];
+      for (int i = 0; i < NX; ++i) c[i] = Rk[RCF::C + i];
+      apply_A(J, k, dx, xn);
+      T tb[NX];
+      apply_B(J, k, du, tb);
+      for (int i = 0; i < NX; ++i) dx[i] = xn[i] + tb[i] + c[i];
+    }
+    if (ln == N)
+      for (int i = 0; i < NX; ++i) dz[i] = dx[i];
+    // stage-parallel part
+    T ap_l = T(1), ad_l = T(1), g_l = T(0);
+    if (own()) {
+      const int k = ln;
+      T* Rk = R(k);
+      for (int i = 0; i < NZ; ++i) g_l += Rk[RCF::GL + i] * dz[i];
+      T z[NZS];
+      load_z(cur, z);
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      T d[NI];
+      int act[NI];
+      row_values(k, z, e, d, act);
+      T adz[NI];
+#pragma unroll
+      for (int r = 0; r < NROW; ++r) {
+        const T v = row_c(r, dz);
+        adz[2 * r] = v;
+        adz[2 * r + 1] = -v;
+      }
+      dz[14] = T(0);
+      adz[JL] = adz[JL + 1] = adz[JL + 2] = T(0);
+      if (lane_active(P, k)) {
+        T htt, hd, gt0, gt1;
+        lane_block(cur, d, htt, hd, gt0, gt1);
+        T gdz = e.gC[0] * dz[0] + e.gC[1] * dz[1] + e.gC[2] * dz[6];
+        T dt = -(hd * gdz + gt0 + mu * gt1) / htt;
+        dz[14] = dt;
+        adz[JL] = gdz + dt;
+        adz[JL + 1] = -gdz + dt;
+        adz[JL + 2] = dt;
+        g_l += sc * P.lane_pen * dt;
+      }
+      for (int i = 0; i < NZS; ++i) S(SSF::DZ + i) = dz[i];
+      for (int j = 0; j < NI; ++j) {
+        if (!act[j]) continue;
+        T s = S(sf(cur) + j), lam = S(SSF::LAM + j);
+        T ds = adz[j] + (d[j] - s);
+        T dl = mu / s - lam - (lam / s) * ds;
+        S(SSF::DS + j) = ds;
+        S(SSF::DLAM + j) = dl;
+        g_l -= mu * ds / s;
+        if (ds < T(0)) ap_l = mr_min(ap_l, -tau * s / ds);
+        if (dl < T(0)) ad_l = mr_min(ad_l, -tau * lam / dl);
+      }
+      if (k >= 1) {  // costate step nu_k + dnu_k = P_k dx_k + p_k
+        for (int i = 0; i < NX; ++i) {
+          T v = Rk[RCF::PV0 + i] + mu * Rk[RCF::PV1 + i];
+          for (int l = 0; l < NX; ++l) v += Rk[RCF::P + pidx(i, l)] * dz[l];
+          S(SSF::DNU + i) = v - S(SSF::NU + i);
+        }
+      }
+    }
+    ap = wmin(w, ap_l);
+    ad = wmin(w, ad_l);
+    gphi = wsum(w, g_l);
+  }
+
+  // ---------------- sweep 4: line-search trial point (writes buffer 1-cur) ----------------
+  MR_SWEEP bool trial(T alpha, bool soc, T& th_t, T& ph_t) {
+    const int nb = 1 - cur;
+    const int k = ln;
+    T z[NZS], zt[NZS], zpl[NZS];
+    load_z(cur, z);
+    for (int i = 0; i < NZS; ++i) zt[i] = z[i] + alpha * (own() ? S(SSF::DZ + i) : T(0));
+    if (k == 0)
+      for (int i = 0; i < NX; ++i) zt[i] = z[i];  // x_0 fixed
+    if (k >= N) { zt[11] = zt[12] = zt[13] = T(0); }
+    for (int i = 0; i < NZS; ++i) zpl[i] = zt[i];
+    if (soc) {
+      // second-order correction: re-roll the shooting states through the dynamics (sequential)
+      T xr[NX], myx[NX];
+      for (int i = 0; i < NX; ++i) { xr[i] = wbcast(w, z[i], 0); myx[i] = xr[i]; }
+      for (int kk = 0; kk < N; ++kk) {
+        T zz[NZS];
+        for (int i = 0; i < NX; ++i) zz[i] = xr[i];
+        zz[11] = wbcast(w, zpl[11], kk);
+        zz[12] = wbcast(w, zpl[12], kk);
+        zz[13] = wbcast(w, zpl[13], kk);
+        zz[14] = T(0);
+        T xn[NX];
+        faug<T, MODEL>(P, kk, zz, xn);
+        for (int i = 0; i < NX; ++i) xr[i] = xn[i];
+        if (ln == kk + 1)
+          for (int i = 0; i < NX; ++i) myx[i] = xr[i];
+      }
+      if (k >= 1)
+        for (int i = 0; i < NX; ++i) zt[i] = myx[i];
+    }
+    T ztn[NX];
+    for (int i = 0; i < NX; ++i) ztn[i] = wshfl(w, zt[i], nxt());
+    T th_l = T(0), f_l = T(0), lg_l = T(0);
+    int ok_l = 1;
+    if (own()) {
+      Err<T> e, ep;
+      errors(I, zt[0], zt[1], zt[6], e, false);
+      T d[NI], dp[NI];
+      int act[NI];
+      row_values(k, zt, e, d, act);
+      if (soc) {
+        errors(I, zpl[0], zpl[1], zpl[6], ep, false);
+        int actp[NI];
+        row_values(k, zpl, ep, dp, actp);
+      }
+      for (int j = 0; j < NI; ++j) {
+        if (!act[j]) continue;
+        T st = S(sf(cur) + j) + alpha * S(SSF::DS + j);
+        if (soc) st += d[j] - dp[j];
+        if (!(st > T(0))) ok_l = 0;
+        S(sf(nb) + j) = st;
+        th_l += mr_abs(d[j] - st);
+        lg_l += mr_log(st > T(0) ? st : T(1));
+      }
+      f_l += stage_cost(P, I, k, zt, e, sc, (T*)nullptr, (T*)nullptr);
+      if (lane_active(P, k)) f_l += sc * P.lane_pen * zt[14];
+      if (k < N && !soc) {
+        T xn[NX];
+        faug<T, MODEL>(P, k, zt, xn);
+        for (int i = 0; i < NX; ++i) th_l += mr_abs(xn[i] - ztn[i]);
+      }
+      for (int i = 0; i < NZS; ++i) S(zf(nb) + i) = zt[i];
+    }
+    th_t = wsum(w, th_l);
+    T fv = wsum(w, f_l), lg = wsum(w, lg_l);
+    int ok = wmin(w, ok_l);
+    ph_t = fv - mu * lg;
+    if (!(th_t == th_t) || !(ph_t == ph_t)) ok = 0;
+    return ok != 0;
+  }
+
+  MR_HD bool filter_ok(T th, T ph) const {
+    for (int i = 0; i < FMAX; ++i)
+      if (i < nfilt && th >= filt_th[i] && ph >= filt_ph[i]) return false;
+    return true;
+  }
+  MR_HD void filter_add(T th, T ph) {
+    if (nfilt < FMAX) {
+      for (int i = 0; i < FMAX; ++i)
+        if (i == nfilt) { filt_th[i] = th; filt_ph[i] = ph; }
+      nfilt++;
+    } else {
+      for (int i = 0; i < FMAX - 1; ++i) { filt_th[i] = filt_th[i + 1]; filt_ph[i] = filt_ph[i + 1]; }
+      filt_th[FMAX - 1] = th;
+      filt_ph[FMAX - 1] = ph;
+    }
+  }
+
+  MR_HD T lane_violation() const {
+    T v = T(0);
+    if (P.lane && own() && ln >= 1) v = S(zf(cur) + 14);
+    return wmax(w, v);
+  }
+
+  // ---------------- the IPM loop (wave-uniform control) ----------------
+  MR_HD SolveOut solve() {
+    const T kappa_eps = T(10), kappa_mu = T(0.2), theta_mu = T(1.5);
+    const T mu_min = P.tol / T(10);
+    const T s_phi = T(2.3), s_theta = T(1.1), delta_sw = T(1), eta = T(1e-4), g_th = T(1e-5), g_ph = T(1e-5);
+    SolveOut out{2, 0, 0.0, 0.0};
+    T mu_prev = mu;
+    int acc_count = 0;
+    int it = 0;
+    for (it = 0;; ++it) {
+      eval_sweep(mu_prev);
+      T kkt = kkt_error(T(0));
+      out.kkt = (double)kkt;
+      out.obj = (double)(fval / sc);
+      if (!(kkt == kkt) || !(fval == fval)) { out.status = 3; break; }
+      if (kkt <= P.tol) { out.status = 0; break; }
+      if (P.acc_iter > 0) {
+        acc_count = (kkt <= P.acc_tol) ? acc_count + 1 : 0;
+        if (acc_count >= P.acc_iter) { out.status = 1; break; }
+      }
+      if (it >= P.max_iter) { out.status = 2; break; }
+      T mu_old = mu;
+      while (kkt_error(mu) <= kappa_eps * mu && mu > mu_min) {
+        T m1 = kappa_mu * mu, m2 = mr_exp(theta_mu * mr_log(mu));
+        mu = mr_max(mu_min, mr_min(m1, m2));
+      }
+      if (mu != mu_old) nfilt = 0;
+      T delta = T(0);
+      bool first = true, fact_ok = false;
+      for (int tries = 0; tries < 60; ++tries) {
+        if (riccati(delta)) { fact_ok = true; break; }
+        if (first) {
+          delta = delta_last == T(0) ? T(1e-4) : mr_max(T(1e-20), delta_last / T(3));
+          first = false;
+        } else {
+          delta *= (delta_last == T(0) ? T(100) : T(8));
+        }
+        if (delta > T(1e40)) break;
+      }
+      if (!fact_ok) { out.status = 3; break; }
+      if (delta > T(0)) delta_last = delta;
+      T ap, ad, gphi;
+      forward(ap, ad, gphi);
+      const T th = theta, ph = fval - mu * logs;
+      const T th_pow = mr_exp(s_theta * mr_log(mr_max(th, T(1e-30))));
+      T a_min;
+      if (gphi < T(0)) {
+        T t1 = g_ph * th / (-gphi);
+        T t2 = delta_sw * th_pow / mr_exp(s_phi * mr_log(-gphi));
+        a_min = T(0.05) * mr_min(g_th, mr_min(t1, t2));
+      } else {
+        a_min = T(0.05) * g_th;
+      }
+      T alpha = ap;
+      bool accepted = false, ftype = false;
+      int nls = 0;
+      while (alpha >= a_min) {
+        for (int pass = 0; pass < 2 && !accepted; ++pass) {
+          bool soc = pass == 1;
+          T th_t, ph_t;
+          bool ok = trial(alpha, soc, th_t, ph_t);
+          if (ok) ok = th_t <= theta_max && filter_ok(th_t, ph_t);
+          if (ok) {
+            bool sw = gphi < T(0) && alpha * mr_exp(s_phi * mr_log(-gphi)) > delta_sw * th_pow;
+            if (th <= theta_min && sw) {
+              ok = ph_t <= ph + eta * alpha * gphi + T(1e-14) * mr_abs(ph);
+              ftype = true;
+            } else {
+              ok = th_t <= (T(1) - g_th) * th || ph_t <= ph - g_ph * th + T(1e-14) * mr_abs(ph);
+              ftype = false;
+            }
+          }
+          if (ok) { accepted = true; break; }
+          if (!(nls == 0 && !soc && th_t >= th)) break;
+        }
+        if (accepted) break;
+        alpha *= T(0.5);
+        nls++;
+      }
+      if (!accepted) {
+        alpha = mr_max(alpha, a_min);
+        T th_t, ph_t;
+        trial(alpha, false, th_t, ph_t);
+        ftype = false;
+      }
+      if (!ftype) filter_add((T(1) - g_th) * th, ph - g_ph * th);
+      if (trace && ln == 0 && it < trace_cap) {
+        double* tr = trace + 8 * it;
+        tr[0] = (double)kkt; tr[1] = (double)mu; tr[2] = (double)alpha; tr[3] = (double)ad;
+        tr[4] = (double)delta; tr[5] = (double)th; tr[6] = (double)ph; tr[7] = (double)(accepted ? nls : -1);
+      }
+      alpha_p = alpha;
+      alpha_d = ad;
+      mu_prev = mu;
+      cur = 1 - cur;
+      wsync(w);  // new iterate buffer written by every lane before the next evaluation
+    }
+    out.iters = it;
+    if (trace && ln == 0 && it < trace_cap) {
+      double* tr = trace + 8 * it;
+      tr[0] = (double)out.kkt; tr[1] = (double)fval; tr[2] = (double)theta; tr[3] = (double)stat_max;
+      tr[4] = (double)pr_max; tr[5] = (double)sc; tr[6] = (double)mu; tr[7] = 1000.0 + out.status;
+    }
+    return out;
+  }
+};
+
+// Per-instance driver: lane `w.lane` of the wave that solves instance i of the batch.
+template <typename T, int MODEL>
+MR_HD void solve_instance_wave(const ProbParams<T>& P, const mr_inputs& in, const mr_outputs& out, int64_t B,
+                               int64_t i, T* ws, T* lds, Wv w) {
+  const int N = P.N;
+  Inst<T> I;
+  const double X0 = in.state0[0 * B + i], Y0 = in.state0[1 * B + i];
+  const double s0 = in.s0[i];
+  I.x0[0] = T(0);
+  I.x0[1] = T(0);
+  for (int j = 2; j < 6; ++j) I.x0[j] = T(in.state0[j * B + i]);
+  double thr0 = in.state0[6 * B + i], st0 = in.state0[7 * B + i];
+  I.has_thr0 = (thr0 == thr0);
+  I.has_steer0 = (st0 == st0);
+  I.thr0 = I.has_thr0 ? T(thr0) : T(0);
+  I.steer0 = I.has_steer0 ? T(st0) : T(0);
+  double cxd[5], cyd[5], ax[5], ay[5];
+  for (int j = 0; j < 5; ++j) { cxd[j] = in.cx[j * B + i]; cyd[j] = in.cy[j * B + i]; }
+  taylor_shift4(cxd, s0, ax);
+  taylor_shift4(cyd, s0, ay);
+  ax[0] -= X0;
+  ay[0] -= Y0;
+  for (int j = 0; j < 5; ++j) { I.ax[j] = T(ax[j]); I.ay[j] = T(ay[j]); }
+  I.max_err = T(in.max_error[i]);
+  I.alpha_c = T(in.runtime[0 * B + i]);
+  I.d_max = T(in.runtime[1 * B + i]);
+  I.q_vy = T(in.runtime[2 * B + i]);
+  I.n = (int)in.runtime[3 * B + i];
+  if (I.n < 1) I.n = 1;
+  I.beta = T(in.runtime[4 * B + i]);
+  WaveSolver<T, MODEL> S(P, I, w, ws, lds);
+  if (out.trace && out.trace_instance == i) { S.trace = out.trace; S.trace_cap = out.trace_cap; }
+  S.init(in.u_init ? in.u_init + i : nullptr, B);
+  SolveOut r = S.solve();
+  const T viol = S.lane_violation();
+  // outputs (the ret tuple of control/MPC.py:166-171), lane k writes stage k, global coordinates
+  if (S.own()) {
+    const int k = w.lane;
+    T z[NZS];
+    S.load_z(S.cur, z);
+    out.X[(0 * (N + 1) + k) * B + i] = (double)z[0] + X0;
+    out.X[(1 * (N + 1) + k) * B + i] = (double)z[1] + Y0;
+    for (int j = 2; j < 6; ++j) out.X[(j * (N + 1) + k) * B + i] = (double)z[j];
+    out.S[k * B + i] = (double)z[6] + s0;
+    if (k < N) {
+      out.U[(0 * N + k) * B + i] = (double)z[11];
+      out.U[(1 * N + k) * B + i] = (double)z[12];
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      out.eC[k * B + i] = (double)e.eC;
+      out.eL[k * B + i] = (double)e.eL;
+    }
+  }
+  if (P.lane && (r.status == 0 || r.status == 1) && (double)viol > 1e-6) r.status = MR_STATUS_LANE_INFEASIBLE;
+  if (w.lane == 0) {
+    out.status[i] = r.status;
+    out.iters[i] = r.iters;
+    if (out.obj) out.obj[i] = r.obj - (double)P.lambda_s * s0;
+    if (out.kkt) out.kkt[i] = r.kkt;
+  }
+}
+
+}  // namespace mr

@@ -1,0 +1,183 @@
+// Wavefront primitives of the wave-per-instance solver (mr_wave.h).
+//
+// gfx950: one 64-lane wavefront = one workgroup = one MPC instance.  Cross-lane
+// values move with ds_bpermute / v_readlane; LDS ordering inside the wave is a
+// workgroup barrier (single-wave workgroup).
+//
+// Host (g++, TEST HARNESS ONLY): the same SPMD source runs as 64 cooperative
+// fibers per instance (ucontext), every primitive a rendezvous of the 64 fibers,
+// so the CPU test suite executes exactly the kernel's code path.  Reductions use
+// the same butterfly order on both sides (bitwise-identical sums given identical
+// inputs).  Every primitive must be reached by all 64 lanes (wave-uniform control
+// flow), as on the device where an inactive source lane would read garbage.
+#pragma once
+#include "mr_common.h"
+
+#if !MR_DEVICE_BUILD
+#include <ucontext.h>
+#include <stdlib.h>
+#include <string.h>
+#endif
+
+namespace mr {
+
+constexpr int WL = 64;  // lanes per instance
+
+#if MR_DEVICE_BUILD
+
+struct Wv {
+  int lane;
+};
+
+__device__ __forceinline__ void wsync(const Wv&) { __syncthreads(); }
+
+__device__ __forceinline__ float wshfl(const Wv&, float v, int src) { return __shfl(v, src, 64); }
+__device__ __forceinline__ double wshfl(const Wv&, double v, int src) { return __shfl(v, src, 64); }
+__device__ __forceinline__ int wshfl(const Wv&, int v, int src) { return __shfl(v, src, 64); }
+__device__ __forceinline__ float wxor(const Wv&, float v, int m) { return __shfl_xor(v, m, 64); }
+__device__ __forceinline__ double wxor(const Wv&, double v, int m) { return __shfl_xor(v, m, 64); }
+__device__ __forceinline__ int wxor(const Wv&, int v, int m) { return __shfl_xor(v, m, 64); }
+
+// value of lane src (src wave-uniform): v_readlane, result lands in an SGPR
+__device__ __forceinline__ int wbcast(const Wv&, int v, int src) { return __builtin_amdgcn_readlane(v, src); }
+__device__ __forceinline__ float wbcast(const Wv&, float v, int src) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), src));
+}
+__device__ __forceinline__ double wbcast(const Wv&, double v, int src) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), src);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+template <typename T>
+__device__ __forceinline__ T wsum(const Wv& w, T v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = v + wxor(w, v, m);
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ T wmax(const Wv& w, T v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) { T o = wxor(w, v, m); v = o > v ? o : v; }
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ T wmin(const Wv& w, T v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) { T o = wxor(w, v, m); v = o < v ? o : v; }
+  return v;
+}
+
+#else  // host fiber emulation -------------------------------------------------------------
+
+struct HostWave {
+  ucontext_t main_ctx;
+  ucontext_t ctx[WL];
+  char* stacks = nullptr;
+  int cur = 0, arrived = 0, done = 0;
+  int fin[WL];
+  alignas(16) unsigned char buf[WL][8];
+  void (*body)(HostWave*, int, void*) = nullptr;
+  void* arg = nullptr;
+
+  void barrier() {
+    if (++arrived == WL) {
+      arrived = 0;
+      return;
+    }
+    const int me = cur;
+    cur = (cur + 1) % WL;
+    swapcontext(&ctx[me], &ctx[cur]);
+  }
+};
+
+struct Wv {
+  int lane;
+  HostWave* hw;
+};
+
+inline void wsync(const Wv& w) { w.hw->barrier(); }
+
+template <typename T>
+inline T wshfl(const Wv& w, T v, int src) {
+  memcpy(w.hw->buf[w.lane], &v, sizeof(T));
+  w.hw->barrier();
+  T r;
+  memcpy(&r, w.hw->buf[((src % WL) + WL) % WL], sizeof(T));
+  w.hw->barrier();
+  return r;
+}
+template <typename T>
+inline T wbcast(const Wv& w, T v, int src) { return wshfl(w, v, src); }
+template <typename T>
+inline T wxor(const Wv& w, T v, int m) { return wshfl(w, v, w.lane ^ m); }
+
+// butterfly reductions, same association as the device (own + partner at every level)
+template <typename T, typename Op>
+inline T host_butterfly(const Wv& w, T v, Op op) {
+  memcpy(w.hw->buf[w.lane], &v, sizeof(T));
+  w.hw->barrier();
+  T vals[WL];
+  for (int l = 0; l < WL; ++l) memcpy(&vals[l], w.hw->buf[l], sizeof(T));
+  w.hw->barrier();
+  for (int m = 32; m >= 1; m >>= 1) {
+    T nv[WL];
+    for (int l = 0; l < WL; ++l) nv[l] = op(vals[l], vals[l ^ m]);
+    for (int l = 0; l < WL; ++l) vals[l] = nv[l];
+  }
+  return vals[w.lane];
+}
+template <typename T>
+inline T wsum(const Wv& w, T v) { return host_butterfly(w, v, [](T a, T b) { return a + b; }); }
+template <typename T>
+inline T wmax(const Wv& w, T v) { return host_butterfly(w, v, [](T a, T b) { return b > a ? b : a; }); }
+template <typename T>
+inline T wmin(const Wv& w, T v) { return host_butterfly(w, v, [](T a, T b) { return b < a ? b : a; }); }
+
+// Run body(hw, lane, arg) as 64 fibers to completion.
+inline void host_wave_run(HostWave& hw, void (*body)(HostWave*, int, void*), void* arg) {
+  const size_t ss = 512 * 1024;
+  hw.stacks = (char*)malloc(ss * WL);
+  hw.body = body;
+  hw.arg = arg;
+  hw.cur = hw.arrived = hw.done = 0;
+  struct Entry {
+    static void run(int lo, int hi) {
+      HostWave* h = (HostWave*)(((uintptr_t)(unsigned)hi << 32) | (uintptr_t)(unsigned)lo);
+      const int lane = h->cur;
+      h->body(h, lane, h->arg);
+      h->fin[lane] = 1;
+      h->done++;
+    }
+  };
+  const uintptr_t p = (uintptr_t)&hw;
+  for (int l = 0; l < WL; ++l) {
+    hw.fin[l] = 0;
+    getcontext(&hw.ctx[l]);
+    hw.ctx[l].uc_stack.ss_sp = hw.stacks + ss * l;
+    hw.ctx[l].uc_stack.ss_size = ss;
+    hw.ctx[l].uc_link = &hw.main_ctx;
+    makecontext(&hw.ctx[l], (void (*)())Entry::run, 2, (int)(unsigned)(p & 0xffffffffu), (int)(unsigned)(p >> 32));
+  }
+  // Fiber 0 starts; barriers rotate through (and thereby start) the others.  Control comes back
+  // here only when a fiber returns: then every other fiber has passed its last barrier (uniform
+  // barrier sequence) or has not started, and may simply be resumed.
+  hw.cur = WL - 1;
+  while (hw.done < WL) {
+    int next = -1;
+    for (int l = 0; l < WL; ++l) {
+      const int c = (hw.cur + 1 + l) % WL;
+      if (!hw.fin[c]) { next = c; break; }
+    }
+    if (next < 0) break;
+    hw.cur = next;
+    swapcontext(&hw.main_ctx, &hw.ctx[next]);
+  }
+  free(hw.stacks);
+  hw.stacks = nullptr;
+}
+
+#endif
+
+}  // namespace mr
