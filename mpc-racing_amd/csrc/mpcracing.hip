@@ -43,7 +43,7 @@ __global__ __launch_bounds__(WL, MR_WAVES_PER_SIMD) void mr_wave_kernel(ProbPara
   __shared__ T lds[LDS_WORDS];
   const int i = blockIdx.x;
   Wv w{(int)threadIdx.x};
-  solve_instance_wave<T, MODEL>(P, in, out, B, i, ws + (int64_t)i * WS_WORDS, lds, w);
+  solve_instance_wave<T, MODEL>(P, in, out, B, i, (MR_GLOBAL T*)(ws + (int64_t)i * WS_WORDS), (MR_LDS T*)lds, w);
 }
 
 static size_t ws_bytes_per_instance(const mr_config& c) {

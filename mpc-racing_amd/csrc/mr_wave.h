@@ -22,10 +22,20 @@
 
 // The sweeps are separate (non-inlined) device functions so each gets its own register
 // allocation; only the small wave-uniform iteration state is live across the calls.
-#if MR_DEVICE_BUILD
+#if MR_DEVICE_BUILD && defined(MR_SWEEP_INLINE)
+#define MR_SWEEP __device__ __forceinline__
+#define MR_CLOCK() ((unsigned long long)__builtin_amdgcn_s_memtime())
+#elif MR_DEVICE_BUILD
 #define MR_SWEEP __device__ __attribute__((noinline))
+#define MR_CLOCK() ((unsigned long long)__builtin_amdgcn_s_memtime())
 #else
 #define MR_SWEEP inline
+#define MR_CLOCK() 0ull
+#endif
+#if MR_DEVICE_BUILD
+#define MR_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)
+#else
+#define MR_SCHED_BARRIER() ((void)0)
 #endif
 
 namespace mr {
@@ -39,14 +49,16 @@ struct SSF {
 struct RCF {
   enum {
     H = 0, G0 = H + NH, G1 = G0 + NZ, GL = G1 + NZ, J = GL + NZ, C = J + 48, P = C + NX, PV0 = P + NP,
-    PV1 = PV0 + NX, K = PV1 + NX, K0 = K + NU * NX, K1 = K0 + NU, NF = K1 + NU
+    PV1 = PV0 + NX, K = PV1 + NX, K0 = K + NU * NX, K1 = K0 + NU, ACL = K1 + NU, FF = ACL + NX * NX,
+    NF = FF + NX
   };
 };
-constexpr int RC_STRIDE = 336;
+constexpr int RC_STRIDE = 468;
 static_assert(RCF::NF <= RC_STRIDE, "record");
 constexpr int64_t WS_WORDS = (int64_t)SSF::NF * WL + (int64_t)RC_STRIDE * WL;
-constexpr int LX_OFF = 0, LQ_OFF = 11 * 16, LW_OFF = LQ_OFF + 16 * 16, LP_OFF = LW_OFF + 11 * 4;
-constexpr int LDS_WORDS = LP_OFF + 11 * 12;
+constexpr int LDS_LD = 17;  // padded row of the 16 x 16 LDS tiles
+constexpr int LX_OFF = 0, LP_OFF = 16 * LDS_LD, LDX_OFF = 32 * LDS_LD;
+constexpr int LDS_WORDS = LDX_OFF + WL * 12;
 
 // lower-triangular solves with L packed (00,10,11,20,21,22) as produced by chol3
 template <typename T>
@@ -90,14 +102,46 @@ MR_HD void row_bounds(const ProbParams<T>& P, const Inst<T>& I, int k, int r, in
 template <typename T>
 MR_HD T row_c(int r, const T* z) { return RN(r) == 1 ? z[RI(r, 0)] : z[RI(r, 0)] - z[RI(r, 1)]; }
 
+// 3x3 Cholesky with reciprocal pivots (3 divisions instead of one per substitution step)
+template <typename T>
+MR_HD bool chol3r(const T* R, T* L, T* iv) {
+  if (!(R[0] > T(0))) return false;
+  const T l00 = mr_sqrt(R[0]);
+  iv[0] = T(1) / l00;
+  const T l10 = R[1] * iv[0], l20 = R[2] * iv[0];
+  const T d1 = R[3] - l10 * l10;
+  if (!(d1 > T(0))) return false;
+  const T l11 = mr_sqrt(d1);
+  iv[1] = T(1) / l11;
+  const T l21 = (R[4] - l20 * l10) * iv[1];
+  const T d2 = R[5] - l20 * l20 - l21 * l21;
+  if (!(d2 > T(0))) return false;
+  const T l22 = mr_sqrt(d2);
+  iv[2] = T(1) / l22;
+  L[0] = l00; L[1] = l10; L[2] = l11; L[3] = l20; L[4] = l21; L[5] = l22;
+  return true;
+}
+template <typename T>
+MR_HD void lsolve3r(const T* L, const T* iv, T* b) {
+  b[0] = b[0] * iv[0];
+  b[1] = (b[1] - L[1] * b[0]) * iv[1];
+  b[2] = (b[2] - L[3] * b[0] - L[4] * b[1]) * iv[2];
+}
+template <typename T>
+MR_HD void ltsolve3r(const T* L, const T* iv, T* b) {
+  b[2] = b[2] * iv[2];
+  b[1] = (b[1] - L[4] * b[2]) * iv[1];
+  b[0] = (b[0] - L[1] * b[1] - L[3] * b[2]) * iv[0];
+}
+
 template <typename T, int MODEL>
 struct WaveSolver {
   const ProbParams<T>& P;
   const Inst<T>& I;
   Wv w;
-  T* ss;
-  T* rc;
-  T* lds;
+  MR_GLOBAL T* ss;
+  MR_GLOBAL T* rc;
+  MR_LDS T* lds;
   int N, ln;
   // wave-uniform iteration state
   int cur;
@@ -111,11 +155,11 @@ struct WaveSolver {
   double* trace = nullptr;
   int trace_cap = 0;
 
-  MR_HD WaveSolver(const ProbParams<T>& P_, const Inst<T>& I_, Wv w_, T* ws, T* lds_)
+  MR_HD WaveSolver(const ProbParams<T>& P_, const Inst<T>& I_, Wv w_, MR_GLOBAL T* ws, MR_LDS T* lds_)
       : P(P_), I(I_), w(w_), ss(ws), rc(ws + (int64_t)SSF::NF * WL), lds(lds_), N(P_.N), ln(w_.lane) {}
 
-  MR_HD T& S(int f) const { return ss[f * WL + ln]; }
-  MR_HD T* R(int k) const { return rc + (int64_t)k * RC_STRIDE; }
+  MR_HD MR_GLOBAL T& S(int f) const { return ss[f * WL + ln]; }
+  MR_HD MR_GLOBAL T* R(int k) const { return rc + (int64_t)k * RC_STRIDE; }
   MR_HD bool own() const { return ln <= N; }
   MR_HD int zf(int b) const { return b ? SSF::Z1 : SSF::Z0; }
   MR_HD int sf(int b) const { return b ? SSF::S1 : SSF::S0; }
@@ -252,7 +296,7 @@ struct WaveSolver {
       znext[i] = wshfl(w, z[i], nxt());
     }
     if (own()) {
-      T* Rk = R(k);
+      MR_GLOBAL T* Rk = R(k);
       T H[NH], g0[NZ], g1[NZ], gl[NZ], st[NZ];
       for (int i = 0; i < NH; ++i) H[i] = T(0);
       for (int i = 0; i < NZ; ++i) { g0[i] = g1[i] = gl[i] = st[i] = T(0); }
@@ -387,163 +431,238 @@ struct WaveSolver {
     return mr_max(mr_max(stat_max / sd, pr_max), cerr / scm);
   }
 
-  // ---------------- sweep 2: Riccati factorisation (backward; lane = matrix row) ----------------
-  //   X = [P' E | P' c + p0' | p1']          (11 x 16, row r on lane r)
-  //   Q = H + E^T X (+ delta I), q0 | q1     (14 x 16, row a on lane a)
-  //   W = L^{-1} Q_ux with L L^T = Q_uu;  P = Q_xx - W^T W;  K = -L^{-T} W
-  MR_SWEEP bool riccati(T delta) {
-    const int r = ln;
-    T* LX = lds + LX_OFF;
-    T* LQ = lds + LQ_OFF;
-    T* LW = lds + LW_OFF;
-    T* LP = lds + LP_OFF;
-    T Prow[NX], p0r = T(0), p1r = T(0);
-    for (int j = 0; j < NX; ++j) Prow[j] = T(0);
-    if (r < NX) {
-      T* Rn = R(N);
-      for (int j = 0; j < NX; ++j) Prow[j] = Rn[RCF::H + hidx(r, j)] + (r == j ? delta : T(0));
-      p0r = Rn[RCF::G0 + r];
-      p1r = Rn[RCF::G1 + r];
-      for (int j = r; j < NX; ++j) Rn[RCF::P + pidx(r, j)] = Prow[j];
-      Rn[RCF::PV0 + r] = p0r;
-      Rn[RCF::PV1 + r] = p1r;
+  // D-register row map of the 16x16x4 MFMA (mr_wave_prims.h) and its inverse
+  static MR_HD constexpr int drow(int g, int v) { return sizeof(T) == 8 ? g + 4 * v : 4 * g + v; }
+  static MR_HD constexpr int dgrp(int a) { return sizeof(T) == 8 ? (a & 3) : (a >> 2); }
+  static MR_HD constexpr int dreg(int a) { return sizeof(T) == 8 ? (a >> 2) : (a & 3); }
+
+  // Entry (i, j) of the 16 x 16 stage map E^ of stage k:
+  //   rows 0..10 = [A | B | 0 | c] of x_{k+1} = A x + B u + c (columns 0..10 x, 11..13 u, 14 c);
+  //   row 11 routes p0 into column 14, row 12 routes p1 into column 15.
+  // Entry (i, j) of E^: record index (data entries: Jacobian or defect) or constant 0/1
+  static MR_HD void ehat_src(int k, int i, int j, int& idx, bool& data, T& cst) {
+    const int jj = j < 6 ? j : (j == 11 ? 6 : (j == 12 ? 7 : -1));
+    const bool cdef = (i < NX) & (j == 14);
+    const bool jac = (i < 6) & (jj >= 0);
+    idx = cdef ? RCF::C + i : (jac ? RCF::J + i * 8 + jj : 0);
+    data = cdef | jac;
+    const bool one = ((i == 6) & ((j == 6) | (j == 13))) | ((i == 7) & (j == 11)) | ((i == 8) & (j == 12)) |
+                     ((i == 9) & (j == (k > 0 ? 9 : 11))) | ((i == 10) & (j == (k > 0 ? 10 : 12))) |
+                     ((i == 11) & (j == 14)) | ((i == 12) & (j == 15));
+    cst = one ? T(1) : T(0);
+  }
+
+  // Per-lane MFMA operands of stage k (lane = (g, c) = (lane >> 4, lane & 15)):
+  //   eb[s] = E^[4s+g][c]                           B fragment of X = P^ E^ and A fragment of E^T X
+  //   hc[v] = (H + delta I | g0 | g1)[drow(g,v)][c]  C input of Q
+  //   ab    = B[c][g] = E^[c][11+g]                 A fragment of B K
+  //   ac[v] = (A | 0 | c)[drow(g,v)][c]             C input of the closed-loop map
+  // frag_load issues the 13 record gathers unconditionally (clamped indices) one stage ahead;
+  // frag_finish applies the selects when the stage is factorised, so no load is sunk into a
+  // lane-divergent branch (which would wait for it on the spot).
+  static MR_HD void frag_load(const MR_GLOBAL T* Rk, int k, int lane, T* raw) {
+    const int g = lane >> 4, c = lane & 15;
+    int idx;
+    bool data;
+    T cst;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) { ehat_src(k, 4 * s + g, c, idx, data, cst); raw[s] = Rk[idx]; }
+    ehat_src(k, c, NX + g, idx, data, cst);
+    raw[4] = Rk[idx];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int a = drow(g, v);
+      const int a_ = a < NZ ? a : 0;
+      raw[5 + v] = Rk[c < NZ ? RCF::H + hidx(a_, c) : (c == 14 ? RCF::G0 + a_ : RCF::G1 + a_)];
+      ehat_src(k, a, c, idx, data, cst);
+      raw[9 + v] = Rk[idx];
     }
+  }
+  static MR_HD void frag_finish(int k, int lane, T delta, const T* raw, T* eb, T* hc, T& ab, T* ac) {
+    const int g = lane >> 4, c = lane & 15;
+    int idx;
+    bool data;
+    T cst;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) { ehat_src(k, 4 * s + g, c, idx, data, cst); eb[s] = data ? raw[s] : cst; }
+    ehat_src(k, c, NX + g, idx, data, cst);
+    ab = ((c < NX) & (g < NU)) ? (data ? raw[4] : cst) : T(0);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int a = drow(g, v);
+      hc[v] = a < NZ ? raw[5 + v] + (a == c ? delta : T(0)) : T(0);
+      ehat_src(k, a, c, idx, data, cst);
+      ac[v] = ((a < NX) & ((c < NX) | (c == 14))) ? (data ? raw[9 + v] : cst) : T(0);
+    }
+  }
+
+  // ---------------- sweep 2: Riccati factorisation on the matrix cores ----------------
+  // Backward over stages, with P^ = [P' | p0' | p1'] (cost-to-go of stage k+1) kept in LDS:
+  //   X    = P^ E^                        4 x v_mfma 16x16x4  (= [P'A  P'B | P'c + p0' | p1'])
+  //   Q    = (H + dI | g0 | g1) + E^T X   4 x v_mfma          (E^'s B fragment is E^T's A fragment)
+  //   Q_uu = L L^T (3x3, wave-uniform),   W = L^{-1} Q_u.     (one column per lane)
+  //   P^   = Q_x. - W^T W                 1 x v_mfma          (upper triangle mirrored)
+  //   K = -L^{-T} W_x,  k0 | k1 = -L^{-T} w0 | w1, and the closed-loop map for the forward pass
+  //   A + B K | B (k0 + mu k1) + c        1 x v_mfma
+  // Stage k-1's record is gathered (13 loads per lane) while stage k is factorised.
+  MR_SWEEP bool riccati(T delta, T mu) {
+    const int l = ln, N = this->N, g = l >> 4, c = l & 15;
+    const Wv w = this->w;
+    MR_GLOBAL T* const rcb = rc;
+    MR_LDS T* const LP = lds + LP_OFF;
+    MR_LDS T* const LX = lds + LX_OFF;
+    auto R = [rcb](int k) { return rcb + (int64_t)k * RC_STRIDE; };
+    for (int q = l; q < 16 * LDS_LD; q += WL) LP[q] = T(0);
+    wsync_lds(w);
+    if (l < NX) {  // terminal cost-to-go: P_N = H_N,xx + delta I, p_N = g_N
+      MR_GLOBAL T* Rn = R(N);
+      for (int j = 0; j < NX; ++j) {
+        const T v = Rn[RCF::H + hidx(l, j)] + (l == j ? delta : T(0));
+        LP[l * LDS_LD + j] = v;
+        if (j >= l) Rn[RCF::P + pidx(l, j)] = v;
+      }
+      const T p0 = Rn[RCF::G0 + l], p1 = Rn[RCF::G1 + l];
+      LP[l * LDS_LD + 11] = p0;
+      LP[l * LDS_LD + 12] = p1;
+      Rn[RCF::PV0 + l] = p0;
+      Rn[RCF::PV1 + l] = p1;
+    }
+    wsync_lds(w);
+    T raw_n[13];
+    frag_load(R(N - 1), N - 1, l, raw_n);
     for (int k = N - 1; k >= 0; --k) {
-      T* Rk = R(k);
-      // R1: row r of X (uniform J, c)
-      if (r < NX) {
-        T J[48], c[NX];
-        for (int i = 0; i < 48; ++i) J[i] = Rk[RCF::J + i];
-        for (int i = 0; i < NX; ++i) c[i] = Rk[RCF::C + i];
-        T xr[16];
-        for (int j = 0; j < 6; ++j) {
-          T acc = T(0);
-          for (int l = 0; l < 6; ++l) acc += Prow[l] * J[l * 8 + j];
-          xr[j] = acc;
-        }
-        T a0 = T(0), a1 = T(0);
-        for (int l = 0; l < 6; ++l) { a0 += Prow[l] * J[l * 8 + 6]; a1 += Prow[l] * J[l * 8 + 7]; }
-        xr[6] = Prow[6];
-        xr[7] = T(0);
-        xr[8] = T(0);
-        xr[9] = k > 0 ? Prow[9] : T(0);
-        xr[10] = k > 0 ? Prow[10] : T(0);
-        xr[11] = a0 + Prow[7] + (k == 0 ? Prow[9] : T(0));
-        xr[12] = a1 + Prow[8] + (k == 0 ? Prow[10] : T(0));
-        xr[13] = Prow[6];
-        T v = p0r;
-        for (int l = 0; l < NX; ++l) v += Prow[l] * c[l];
-        xr[14] = v;
-        xr[15] = p1r;
-        for (int j = 0; j < 16; ++j) LX[r * 16 + j] = xr[j];
+      MR_GLOBAL T* Rk = R(k);
+      T eb[4], dq[4], dacl[4], ab;
+      frag_finish(k, l, delta, raw_n, eb, dq, ab, dacl);
+      if (k >= 1) frag_load(R(k - 1), k - 1, l, raw_n);
+      // X = P^ E^  (A fragment s: P^[c][4s+g])
+      T dx[4] = {T(0), T(0), T(0), T(0)};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) wmfma(w, LP[c * LDS_LD + 4 * s + g], eb[s], dx);
+      // B fragments X[4s+g][c]
+      T xb[4];
+      if (sizeof(T) == 8) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) xb[s] = dx[s];  // f64: register s already holds row g + 4s
+      } else {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) LX[(4 * g + v) * LDS_LD + c] = dx[v];
+        wsync_lds(w);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) xb[s] = LX[(4 * s + g) * LDS_LD + c];
       }
-      wsync(w);
-      // R2: row a of Q = H_k + e_a^T X, e_a = column a of E = [A B]
-      T qa[16];
-      for (int b = 0; b < 16; ++b) qa[b] = T(0);
-      if (r < NZ) {
-        const int a = r;
-        const int ja = a < 6 ? a : (a == 11 ? 6 : (a == 12 ? 7 : -1));
-        T e[NX];
-        for (int i = 0; i < 6; ++i) e[i] = ja >= 0 ? Rk[RCF::J + i * 8 + ja] : T(0);
-        e[6] = (a == 6 || a == 13) ? T(1) : T(0);
-        e[7] = a == 11 ? T(1) : T(0);
-        e[8] = a == 12 ? T(1) : T(0);
-        e[9] = (k > 0 ? a == 9 : a == 11) ? T(1) : T(0);
-        e[10] = (k > 0 ? a == 10 : a == 12) ? T(1) : T(0);
-        for (int b = 0; b < 16; ++b) {
-          T acc = T(0);
-          for (int i = 0; i < NX; ++i) acc += e[i] * LX[i * 16 + b];
-          qa[b] = acc;
+      // Q = (H + delta I | g0 | g1) + E^T X
+#pragma unroll
+      for (int s = 0; s < 4; ++s) wmfma(w, eb[s], xb[s], dq);
+      auto qat = [&](int a, int b) { return wbcast(w, dq[dreg(a)], dgrp(a) * 16 + b); };
+      T Rh[6] = {qat(11, 11), qat(11, 12), qat(11, 13), qat(12, 12), qat(12, 13), qat(13, 13)};
+      T L[6], iv[3];
+      if (!chol3r(Rh, L, iv)) return false;  // wave-uniform: same inputs and code on every lane
+      T w0[3] = {qat(11, 14), qat(12, 14), qat(13, 14)};
+      T w1[3] = {qat(11, 15), qat(12, 15), qat(13, 15)};
+      lsolve3r(L, iv, w0);
+      lsolve3r(L, iv, w1);
+      T wc[3] = {wshfl(w, dq[dreg(11)], dgrp(11) * 16 + c), wshfl(w, dq[dreg(12)], dgrp(12) * 16 + c),
+                 wshfl(w, dq[dreg(13)], dgrp(13) * 16 + c)};
+      lsolve3r(L, iv, wc);  // W[:, c]
+      const T wv = g == 0 ? wc[0] : (g == 1 ? wc[1] : (g == 2 ? wc[2] : T(0)));
+      T dw[4] = {T(0), T(0), T(0), T(0)};
+      wmfma(w, wv, wv, dw);  // W^T W
+      // gains: K[:, c] = -L^{-T} W[:, c], feed-forward k0, k1
+      T kc[3] = {wc[0], wc[1], wc[2]}, k0[3] = {w0[0], w0[1], w0[2]}, k1[3] = {w1[0], w1[1], w1[2]};
+      ltsolve3r(L, iv, kc);
+      ltsolve3r(L, iv, k0);
+      ltsolve3r(L, iv, k1);
+      if (g == 0 && c < NX)
+        for (int a = 0; a < NU; ++a) Rk[RCF::K + a * NX + c] = -kc[a];
+      if (l == 0)
+        for (int a = 0; a < NU; ++a) { Rk[RCF::K0 + a] = -k0[a]; Rk[RCF::K1 + a] = -k1[a]; }
+      // closed-loop map (A + B K | B (k0 + mu k1) + c) for the forward recursion
+      const T kg = g == 0 ? kc[0] : (g == 1 ? kc[1] : kc[2]);
+      const T kf = g == 0 ? k0[0] + mu * k1[0] : (g == 1 ? k0[1] + mu * k1[1] : k0[2] + mu * k1[2]);
+      const T kb = g < NU ? (c < NX ? -kg : (c == 14 ? -kf : T(0))) : T(0);
+      wmfma(w, ab, kb, dacl);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int a = drow(g, v);
+        const T pv = dq[v] - dw[v];
+        if (a < NX) {
+          if (c < NX) {
+            Rk[RCF::ACL + a * NX + c] = dacl[v];
+            if (a <= c) {
+              Rk[RCF::P + pidx(a, c)] = pv;
+              LP[a * LDS_LD + c] = pv;
+              LP[c * LDS_LD + a] = pv;
+            }
+          } else if (c == 14) {
+            Rk[RCF::FF + a] = dacl[v];
+            Rk[RCF::PV0 + a] = pv;
+            LP[a * LDS_LD + 11] = pv;
+          } else if (c == 15) {
+            Rk[RCF::PV1 + a] = pv;
+            LP[a * LDS_LD + 12] = pv;
+          }
         }
-        for (int b = 0; b < NZ; ++b) qa[b] += Rk[RCF::H + hidx(a, b)] + (a == b ? delta : T(0));
-        qa[14] += Rk[RCF::G0 + a];
-        qa[15] += Rk[RCF::G1 + a];
-        for (int b = 0; b < 16; ++b) LQ[a * 16 + b] = qa[b];
       }
-      wsync(w);
-      // R3: Q_uu = L L^T (wave-uniform), W column r, new P row r
-      T Rh[6] = {LQ[11 * 16 + 11], LQ[11 * 16 + 12], LQ[11 * 16 + 13],
-                 LQ[12 * 16 + 12], LQ[12 * 16 + 13], LQ[13 * 16 + 13]};
-      T L[6];
-      if (!chol3(Rh, L)) return false;  // uniform: identical inputs and code on every lane
-      T w0[3] = {LQ[11 * 16 + 14], LQ[12 * 16 + 14], LQ[13 * 16 + 14]};
-      T w1[3] = {LQ[11 * 16 + 15], LQ[12 * 16 + 15], LQ[13 * 16 + 15]};
-      lsolve3(L, w0);
-      lsolve3(L, w1);
-      T Wr[3] = {qa[11], qa[12], qa[13]};  // Q_ux[:, r] = Q_xu[r, :] (row r, symmetric)
-      lsolve3(L, Wr);
-      if (r < NX)
-        for (int m = 0; m < 3; ++m) LW[r * 4 + m] = Wr[m];
-      wsync(w);
-      T Pn[NX];
-      for (int j = 0; j < NX; ++j) Pn[j] = T(0);
-      if (r < NX) {
-        for (int j = 0; j < NX; ++j)
-          Pn[j] = qa[j] - (Wr[0] * LW[j * 4 + 0] + Wr[1] * LW[j * 4 + 1] + Wr[2] * LW[j * 4 + 2]);
-        T p0n = qa[14] - (Wr[0] * w0[0] + Wr[1] * w0[1] + Wr[2] * w0[2]);
-        T p1n = qa[15] - (Wr[0] * w1[0] + Wr[1] * w1[1] + Wr[2] * w1[2]);
-        T kr[3] = {Wr[0], Wr[1], Wr[2]};
-        ltsolve3(L, kr);
-        for (int j = r; j < NX; ++j) {
-          Rk[RCF::P + pidx(r, j)] = Pn[j];
-          LP[r * 12 + j] = Pn[j];
-        }
-        Rk[RCF::PV0 + r] = p0n;
-        Rk[RCF::PV1 + r] = p1n;
-        for (int a = 0; a < NU; ++a) Rk[RCF::K + a * NX + r] = -kr[a];
-        if (r == 0) {
-          T k0[3] = {w0[0], w0[1], w0[2]}, k1[3] = {w1[0], w1[1], w1[2]};
-          ltsolve3(L, k0);
-          ltsolve3(L, k1);
-          for (int a = 0; a < NU; ++a) { Rk[RCF::K0 + a] = -k0[a]; Rk[RCF::K1 + a] = -k1[a]; }
-        }
-        p0r = p0n;
-        p1r = p1n;
-      }
-      wsync(w);
-      // symmetric P for the next stage: upper triangle from the owning rows
-      if (r < NX)
-        for (int j = 0; j < NX; ++j) Prow[j] = j >= r ? Pn[j] : LP[j * 12 + r];
+      wsync_lds(w);
     }
-    wsync(w);  // records (P, K) visible to every lane
+    wsync(w);  // records (P, K, closed-loop map) visible to every lane
     return true;
   }
 
   // ---------------- sweep 3: forward substitution, slack/dual steps ----------------
+  //   dx_{k+1} = (A + B K)_k dx_k + f_k with the closed-loop map of the Riccati sweep: lane
+  //   i < 11 owns dx[i], the 11 values are shared with v_readlane, one 11-term dot per step.
+  //   Then stage-parallel: du_k = K_k dx_k + k0 + mu k1, slack/dual steps, costates.
   MR_SWEEP void forward(T& ap, T& ad, T& gphi) {
+    const T mu = this->mu;
     const T tau = mr_max(T(0.99), T(1) - mu);
-    T dx[NX], dz[NZS];
-    for (int i = 0; i < NX; ++i) dx[i] = T(0);
+    T dz[NZS];
     for (int i = 0; i < NZS; ++i) dz[i] = T(0);
-    // sequential part: dz_k = (dx_k, K_k dx_k + k0 + mu k1), dx_{k+1} = A dx + B du + c (wave-uniform)
-    for (int k = 0; k < N; ++k) {
-      const T* Rk = R(k);
-      T du[NU];
-      for (int a = 0; a < NU; ++a) {
-        T v = Rk[RCF::K0 + a] + mu * Rk[RCF::K1 + a];
-        for (int j = 0; j < NX; ++j) v += Rk[RCF::K + a * NX + j] * dx[j];
-        du[a] = v;
+    {
+      const int N = this->N, ln = this->ln;
+      const Wv w = this->w;
+      MR_GLOBAL T* const rcb = rc;
+      MR_LDS T* const LDX = lds + LDX_OFF;
+      auto R = [rcb](int k) { return rcb + (int64_t)k * RC_STRIDE; };
+      const int i = ln < NX ? ln : 0;
+      T dxi = T(0);
+      if (ln < NX) LDX[ln] = T(0);
+      T ar_n[NX], f_n;
+      for (int j = 0; j < NX; ++j) ar_n[j] = R(0)[RCF::ACL + i * NX + j];
+      f_n = R(0)[RCF::FF + i];
+      for (int k = 0; k < N; ++k) {
+        T ar[NX];
+        for (int j = 0; j < NX; ++j) ar[j] = ar_n[j];
+        const T fi = f_n;
+        if (k + 1 < N) {
+          for (int j = 0; j < NX; ++j) ar_n[j] = R(k + 1)[RCF::ACL + i * NX + j];
+          f_n = R(k + 1)[RCF::FF + i];
+        }
+        T dxv[NX];
+        wgather<T, NX>(w, dxi, dxv);
+        T acc = fi;
+        for (int j = 0; j < NX; ++j) acc += ar[j] * dxv[j];
+        dxi = ln < NX ? acc : T(0);
+        if (ln < NX) LDX[(k + 1) * 12 + ln] = dxi;
       }
-      if (ln == k) {
-        for (int i = 0; i < NX; ++i) dz[i] = dx[i];
-        for (int a = 0; a < NU; ++a) dz[NX + a] = du[a];
+      wsync_lds(w);
+      if (ln <= N)
+        for (int j = 0; j < NX; ++j) dz[j] = LDX[ln * 12 + j];
+      if (ln < N) {
+        const MR_GLOBAL T* Rk = R(ln);
+        for (int a = 0; a < NU; ++a) {
+          T v = Rk[RCF::K0 + a] + mu * Rk[RCF::K1 + a];
+          for (int j = 0; j < NX; ++j) v += Rk[RCF::K + a * NX + j] * dz[j];
+          dz[NX + a] = v;
+        }
       }
-      T J[48], c[NX], xn[NX];
-      for (int i = 0; i < 48; ++i) J[i] = Rk[RCF::J + i];
-      for (int i = 0; i < NX; ++i) c[i] = Rk[RCF::C + i];
-      apply_A(J, k, dx, xn);
-      T tb[NX];
-      apply_B(J, k, du, tb);
-      for (int i = 0; i < NX; ++i) dx[i] = xn[i] + tb[i] + c[i];
     }
-    if (ln == N)
-      for (int i = 0; i < NX; ++i) dz[i] = dx[i];
     // stage-parallel part
     T ap_l = T(1), ad_l = T(1), g_l = T(0);
     if (own()) {
       const int k = ln;
-      T* Rk = R(k);
+      MR_GLOBAL T* Rk = R(k);
       for (int i = 0; i < NZ; ++i) g_l += Rk[RCF::GL + i] * dz[i];
       T z[NZS];
       load_z(cur, z);
@@ -701,8 +820,14 @@ struct WaveSolver {
     T mu_prev = mu;
     int acc_count = 0;
     int it = 0;
+    // diagnostics of the trace instance: shader cycles per phase and call counts
+    unsigned long long cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t0 = 0, tstart = trace ? MR_CLOCK() : 0ull;
+#define MR_T0() (t0 = trace ? MR_CLOCK() : 0ull)
+#define MR_T1(slot) (cyc[slot] += trace ? MR_CLOCK() - t0 : 0ull)
     for (it = 0;; ++it) {
+      MR_T0();
       eval_sweep(mu_prev);
+      MR_T1(0);
       T kkt = kkt_error(T(0));
       out.kkt = (double)kkt;
       out.obj = (double)(fval / sc);
@@ -721,8 +846,10 @@ struct WaveSolver {
       if (mu != mu_old) nfilt = 0;
       T delta = T(0);
       bool first = true, fact_ok = false;
+      MR_T0();
       for (int tries = 0; tries < 60; ++tries) {
-        if (riccati(delta)) { fact_ok = true; break; }
+        cyc[6]++;
+        if (riccati(delta, mu)) { fact_ok = true; break; }
         if (first) {
           delta = delta_last == T(0) ? T(1e-4) : mr_max(T(1e-20), delta_last / T(3));
           first = false;
@@ -731,10 +858,13 @@ struct WaveSolver {
         }
         if (delta > T(1e40)) break;
       }
+      MR_T1(1);
       if (!fact_ok) { out.status = 3; break; }
       if (delta > T(0)) delta_last = delta;
       T ap, ad, gphi;
+      MR_T0();
       forward(ap, ad, gphi);
+      MR_T1(2);
       const T th = theta, ph = fval - mu * logs;
       const T th_pow = mr_exp(s_theta * mr_log(mr_max(th, T(1e-30))));
       T a_min;
@@ -752,7 +882,11 @@ struct WaveSolver {
         for (int pass = 0; pass < 2 && !accepted; ++pass) {
           bool soc = pass == 1;
           T th_t, ph_t;
+          MR_T0();
           bool ok = trial(alpha, soc, th_t, ph_t);
+          MR_T1(3);
+          cyc[4]++;
+          if (soc) cyc[5]++;
           if (ok) ok = th_t <= theta_max && filter_ok(th_t, ph_t);
           if (ok) {
             bool sw = gphi < T(0) && alpha * mr_exp(s_phi * mr_log(-gphi)) > delta_sw * th_pow;
@@ -778,7 +912,7 @@ struct WaveSolver {
         ftype = false;
       }
       if (!ftype) filter_add((T(1) - g_th) * th, ph - g_ph * th);
-      if (trace && ln == 0 && it < trace_cap) {
+      if (trace && ln == 0 && it < trace_cap - 1) {
         double* tr = trace + 8 * it;
         tr[0] = (double)kkt; tr[1] = (double)mu; tr[2] = (double)alpha; tr[3] = (double)ad;
         tr[4] = (double)delta; tr[5] = (double)th; tr[6] = (double)ph; tr[7] = (double)(accepted ? nls : -1);
@@ -790,7 +924,14 @@ struct WaveSolver {
       wsync(w);  // new iterate buffer written by every lane before the next evaluation
     }
     out.iters = it;
-    if (trace && ln == 0 && it < trace_cap) {
+#undef MR_T0
+#undef MR_T1
+    if (trace && ln == 0 && trace_cap >= 2) {  // last row: cycles eval, riccati, forward, trial, #trials, #soc, #factorisations, total
+      double* tr = trace + 8 * (trace_cap - 1);
+      for (int q = 0; q < 7; ++q) tr[q] = (double)cyc[q];
+      tr[7] = (double)(trace ? MR_CLOCK() - tstart : 0ull);
+    }
+    if (trace && ln == 0 && it < trace_cap - 1) {
       double* tr = trace + 8 * it;
       tr[0] = (double)out.kkt; tr[1] = (double)fval; tr[2] = (double)theta; tr[3] = (double)stat_max;
       tr[4] = (double)pr_max; tr[5] = (double)sc; tr[6] = (double)mu; tr[7] = 1000.0 + out.status;
@@ -802,7 +943,7 @@ struct WaveSolver {
 // Per-instance driver: lane `w.lane` of the wave that solves instance i of the batch.
 template <typename T, int MODEL>
 MR_HD void solve_instance_wave(const ProbParams<T>& P, const mr_inputs& in, const mr_outputs& out, int64_t B,
-                               int64_t i, T* ws, T* lds, Wv w) {
+                               int64_t i, MR_GLOBAL T* ws, MR_LDS T* lds, Wv w) {
   const int N = P.N;
   Inst<T> I;
   const double X0 = in.state0[0 * B + i], Y0 = in.state0[1 * B + i];

@@ -17,6 +17,18 @@
 #include <ucontext.h>
 #include <stdlib.h>
 #include <string.h>
+#include <cmath>
+#endif
+
+// Address-space qualifiers: keep the workspace in the global and the exchange buffers in the
+// LDS address space through the sweep functions (otherwise every access becomes a flat_* op
+// that waits on both memory counters).
+#if MR_DEVICE_BUILD
+#define MR_GLOBAL __attribute__((address_space(1)))
+#define MR_LDS __attribute__((address_space(3)))
+#else
+#define MR_GLOBAL
+#define MR_LDS
 #endif
 
 namespace mr {
@@ -29,7 +41,17 @@ struct Wv {
   int lane;
 };
 
+// Full sync: LDS and global memory written by any lane visible to every lane (workgroup
+// release/acquire: waits for this wave's outstanding vector-memory operations).
 __device__ __forceinline__ void wsync(const Wv&) { __syncthreads(); }
+// LDS-only sync inside the single-wave workgroup: a wavefront's DS instructions execute in
+// issue order, so a compiler-level barrier is enough; outstanding global loads (prefetches)
+// and stores stay in flight.
+__device__ __forceinline__ void wsync_lds(const Wv&) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 __device__ __forceinline__ float wshfl(const Wv&, float v, int src) { return __shfl(v, src, 64); }
 __device__ __forceinline__ double wshfl(const Wv&, double v, int src) { return __shfl(v, src, 64); }
@@ -48,6 +70,28 @@ __device__ __forceinline__ double wbcast(const Wv&, double v, int src) {
   const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), src);
   const int hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
   return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+// One 16x16x4 MFMA over the wave: D += A * B with lane l holding A[l&15][l>>4] and
+// B[l>>4][l&15]; D row of register v: 4*(l>>4)+v (f32), (l>>4)+4*v (f64); column l&15.
+typedef float mr_f32x4 __attribute__((ext_vector_type(4)));
+typedef double mr_f64x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void wmfma(const Wv&, float a, float b, float* d) {
+  mr_f32x4 c = {d[0], d[1], d[2], d[3]};
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  d[0] = c[0]; d[1] = c[1]; d[2] = c[2]; d[3] = c[3];
+}
+__device__ __forceinline__ void wmfma(const Wv&, double a, double b, double* d) {
+  mr_f64x4 c = {d[0], d[1], d[2], d[3]};
+  c = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+  d[0] = c[0]; d[1] = c[1]; d[2] = c[2]; d[3] = c[3];
+}
+
+// out[i] = value of lane i, i < n (compile-time n): one v_readlane per element
+template <typename T, int n>
+__device__ __forceinline__ void wgather(const Wv& w, T v, T* out) {
+#pragma unroll
+  for (int i = 0; i < n; ++i) out[i] = wbcast(w, v, i);
 }
 
 template <typename T>
@@ -77,7 +121,7 @@ struct HostWave {
   char* stacks = nullptr;
   int cur = 0, arrived = 0, done = 0;
   int fin[WL];
-  alignas(16) unsigned char buf[WL][8];
+  alignas(16) unsigned char buf[WL][16];
   void (*body)(HostWave*, int, void*) = nullptr;
   void* arg = nullptr;
 
@@ -98,6 +142,7 @@ struct Wv {
 };
 
 inline void wsync(const Wv& w) { w.hw->barrier(); }
+inline void wsync_lds(const Wv& w) { w.hw->barrier(); }
 
 template <typename T>
 inline T wshfl(const Wv& w, T v, int src) {
@@ -112,6 +157,35 @@ template <typename T>
 inline T wbcast(const Wv& w, T v, int src) { return wshfl(w, v, src); }
 template <typename T>
 inline T wxor(const Wv& w, T v, int m) { return wshfl(w, v, w.lane ^ m); }
+
+// 16x16x4 MFMA emulation: same lane maps and the same k-ordered fma chain as gfx950
+template <typename T>
+inline void wmfma(const Wv& w, T a, T b, T* d) {
+  memcpy(w.hw->buf[w.lane], &a, sizeof(T));
+  memcpy(w.hw->buf[w.lane] + 8, &b, sizeof(T));
+  w.hw->barrier();
+  const int g = w.lane >> 4, c = w.lane & 15;
+  for (int v = 0; v < 4; ++v) {
+    const int row = sizeof(T) == 8 ? g + 4 * v : 4 * g + v;
+    T acc = d[v];
+    for (int k = 0; k < 4; ++k) {
+      T av, bv;
+      memcpy(&av, w.hw->buf[k * 16 + row], sizeof(T));
+      memcpy(&bv, w.hw->buf[k * 16 + c] + 8, sizeof(T));
+      acc = std::fma(av, bv, acc);
+    }
+    d[v] = acc;
+  }
+  w.hw->barrier();
+}
+
+template <typename T, int n>
+inline void wgather(const Wv& w, T v, T* out) {
+  memcpy(w.hw->buf[w.lane], &v, sizeof(T));
+  w.hw->barrier();
+  for (int i = 0; i < n; ++i) memcpy(&out[i], w.hw->buf[i], sizeof(T));
+  w.hw->barrier();
+}
 
 // butterfly reductions, same association as the device (own + partner at every level)
 template <typename T, typename Op>

@@ -1,0 +1,62 @@
+"""Developer probe: per-phase shader cycles of single instances (trace instance, last
+trace row) and B=1 wall latency; writes gpurun_out/phase_probe.json."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.abspath(os.path.join(HERE, "..", ".."))
+sys.path.insert(0, os.path.join(REPO, "mpc-racing_amd"))
+from mpcracing import workload as wl  # noqa: E402
+from mpcracing.batch import solver_for_config  # noqa: E402
+
+NAMES = ["eval", "riccati", "forward", "trial", "n_trials", "n_soc", "n_fact", "total"]
+
+
+def one(name, b, i, cap=520):
+    sub = {k: (v[..., i:i + 1].copy() if v is not None else None) for k, v in b.items()}
+    s = solver_for_config(name, 1)
+    out = s.solve(sub, trace_instance=0, trace_cap=cap)
+    torch.cuda.synchronize()
+    lat = []
+    d = s.to_device(sub)
+    o = s.alloc_outputs(1)
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        s.launch(d, o)
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - t)
+    tr = out["trace"].cpu().numpy()
+    it = int(out["iters"][0])
+    row = dict(zip(NAMES, tr[-1].tolist()))
+    row.update(instance=i, iters=it, status=int(out["status"][0]), wall_ms=1e3 * min(lat),
+               cycles_per_iter=row["total"] / max(it, 1))
+    return row
+
+
+def main():
+    names = sys.argv[1].split(",") if len(sys.argv) > 1 else ["C4"]
+    res = {}
+    for name in names:
+        b = wl.make_batch(name)
+        B = b["s0"].shape[0]
+        s = solver_for_config(name, B)
+        o = {k: v.cpu().numpy() for k, v in s.solve(b).items()}
+        it = o["iters"]
+        order = np.argsort(it)
+        picks = [int(order[len(order) // 2]), int(order[-1]), int(order[-2])]
+        res[name] = [one(name, b, i) for i in picks]
+        for r in res[name]:
+            print(name, json.dumps(r), flush=True)
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(REPO, "gpurun_out", "phase_probe.json"), "w") as f:
+        json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
