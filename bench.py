@@ -181,7 +181,7 @@ def main():
                             "failed": int(tot[6]), "lane_infeasible": int(tot[7])},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "mr_solve_kernel", "avg_launch_ms": kavg * 1e3,
+                         "kernel": "mr_wave_kernel", "avg_launch_ms": kavg * 1e3,
                          "alg_bytes_per_launch": alg_bytes},
         }
         line["iters_mean"] = float(iters_sum / B)

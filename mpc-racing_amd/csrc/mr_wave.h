@@ -50,15 +50,16 @@ struct RCF {
   enum {
     H = 0, G0 = H + NH, G1 = G0 + NZ, GL = G1 + NZ, J = GL + NZ, C = J + 48, P = C + NX, PV0 = P + NP,
     PV1 = PV0 + NX, K = PV1 + NX, K0 = K + NU * NX, K1 = K0 + NU, ACL = K1 + NU, FF = ACL + NX * NX,
-    NF = FF + NX
+    JUNK = FF + NX, NF = JUNK + WL
   };
 };
-constexpr int RC_STRIDE = 468;
+constexpr int RC_STRIDE = 532;
 static_assert(RCF::NF <= RC_STRIDE, "record");
 constexpr int64_t WS_WORDS = (int64_t)SSF::NF * WL + (int64_t)RC_STRIDE * WL;
 constexpr int LDS_LD = 17;  // padded row of the 16 x 16 LDS tiles
 constexpr int LX_OFF = 0, LP_OFF = 16 * LDS_LD, LDX_OFF = 32 * LDS_LD;
-constexpr int LDS_WORDS = LDX_OFF + WL * 12;
+constexpr int LJUNK_OFF = LDX_OFF + WL * 12;  // one discard slot per lane (branch-free stores)
+constexpr int LDS_WORDS = LJUNK_OFF + WL;
 
 // lower-triangular solves with L packed (00,10,11,20,21,22) as produced by chol3
 template <typename T>
@@ -154,6 +155,7 @@ struct WaveSolver {
   int me, mi;
   double* trace = nullptr;
   int trace_cap = 0;
+  unsigned long long tsub[4] = {0, 0, 0, 0};  // diagnostics: sub-phase cycles of the trace instance
 
   MR_HD WaveSolver(const ProbParams<T>& P_, const Inst<T>& I_, Wv w_, MR_GLOBAL T* ws, MR_LDS T* lds_)
       : P(P_), I(I_), w(w_), ss(ws), rc(ws + (int64_t)SSF::NF * WL), lds(lds_), N(P_.N), ln(w_.lane) {}
@@ -295,6 +297,7 @@ struct WaveSolver {
       nun[i] = wshfl(w, nuk[i], nxt());
       znext[i] = wshfl(w, z[i], nxt());
     }
+    const unsigned long long te0 = trace ? MR_CLOCK() : 0ull;
     if (own()) {
       MR_GLOBAL T* Rk = R(k);
       T H[NH], g0[NZ], g1[NZ], gl[NZ], st[NZ];
@@ -408,6 +411,7 @@ struct WaveSolver {
       for (int i = 0; i < NH; ++i) Rk[RCF::H + i] = H[i];
       for (int i = 0; i < NZ; ++i) { Rk[RCF::G0 + i] = g0[i]; Rk[RCF::G1 + i] = g1[i]; Rk[RCF::GL + i] = gl[i]; }
     }
+    const unsigned long long te1 = trace ? MR_CLOCK() : 0ull;
     stat_max = wmax(w, st_l);
     pr_max = wmax(w, pr_l);
     theta = wsum(w, th_l);
@@ -420,6 +424,7 @@ struct WaveSolver {
     mi = wsum(w, mi_l);
     me = NX * (N + 1);
     wsync(w);  // stage records visible to every lane before the Riccati sweep
+    if (trace) { tsub[2] += te1 - te0; tsub[3] += MR_CLOCK() - te1; }
   }
 
   MR_HD T kkt_error(T m) const {
@@ -454,45 +459,69 @@ struct WaveSolver {
 
   // Per-lane MFMA operands of stage k (lane = (g, c) = (lane >> 4, lane & 15)):
   //   eb[s] = E^[4s+g][c]                           B fragment of X = P^ E^ and A fragment of E^T X
-  //   hc[v] = (H + delta I | g0 | g1)[drow(g,v)][c]  C input of Q
   //   ab    = B[c][g] = E^[c][11+g]                 A fragment of B K
+  //   hc[v] = (H + delta I | g0 | g1)[drow(g,v)][c]  C input of Q
   //   ac[v] = (A | 0 | c)[drow(g,v)][c]             C input of the closed-loop map
-  // frag_load issues the 13 record gathers unconditionally (clamped indices) one stage ahead;
-  // frag_finish applies the selects when the stage is factorised, so no load is sunk into a
-  // lane-divergent branch (which would wait for it on the spot).
-  static MR_HD void frag_load(const MR_GLOBAL T* Rk, int k, int lane, T* raw) {
+  // The gather plan (record offsets, data/constant/diagonal bits, output targets) depends on
+  // the lane only (k == 0 differs in two constants) and is built once per factorisation;
+  // frag_load issues the 13 gathers unconditionally one stage ahead, frag_finish applies the
+  // selects when the stage is factorised, so no load is sunk into a lane-divergent branch.
+  struct FragPlan {
+    int off[13];
+    unsigned data, one_pos, one_k0, dlt;
+    int st_a[4], st_p[4], lp1[4], lp2[4];  // per D register: record / LDS targets (discard slots if none)
+  };
+  static MR_HD void frag_plan(int lane, FragPlan& fp) {
     const int g = lane >> 4, c = lane & 15;
+    fp.data = fp.one_pos = fp.one_k0 = fp.dlt = 0u;
     int idx;
     bool data;
     T cst;
+    auto put = [&](int q, int i, int j, bool keep) {
+      ehat_src(1, i, j, idx, data, cst);
+      fp.off[q] = idx;
+      if (keep && data) fp.data |= 1u << q;
+      if (keep && cst != T(0)) fp.one_pos |= 1u << q;
+      ehat_src(0, i, j, idx, data, cst);
+      if (keep && cst != T(0)) fp.one_k0 |= 1u << q;
+    };
 #pragma unroll
-    for (int s = 0; s < 4; ++s) { ehat_src(k, 4 * s + g, c, idx, data, cst); raw[s] = Rk[idx]; }
-    ehat_src(k, c, NX + g, idx, data, cst);
-    raw[4] = Rk[idx];
+    for (int s = 0; s < 4; ++s) put(s, 4 * s + g, c, true);
+    put(4, c, NX + g, (c < NX) & (g < NU));
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const int a = drow(g, v);
       const int a_ = a < NZ ? a : 0;
-      raw[5 + v] = Rk[c < NZ ? RCF::H + hidx(a_, c) : (c == 14 ? RCF::G0 + a_ : RCF::G1 + a_)];
-      ehat_src(k, a, c, idx, data, cst);
-      raw[9 + v] = Rk[idx];
+      fp.off[5 + v] = c < NZ ? RCF::H + hidx(a_, c) : (c == 14 ? RCF::G0 + a_ : RCF::G1 + a_);
+      if (a < NZ) fp.data |= 1u << (5 + v);
+      if (a < NZ && a == c) fp.dlt |= 1u << (5 + v);
+      put(9 + v, a, c, (a < NX) & ((c < NX) | (c == 14)));
+      // outputs of D register v: closed-loop map, packed-upper P | p0 | p1, LDS image of P^
+      const int junk_r = RCF::JUNK + lane, junk_l = LJUNK_OFF - LP_OFF + lane;  // lp* index from LP
+      const bool ax = a < NX, up = ax & (c < NX) & (a <= c);
+      fp.st_a[v] = ax & (c < NX) ? RCF::ACL + a * NX + c : (ax & (c == 14) ? RCF::FF + a : junk_r);
+      fp.st_p[v] = up ? RCF::P + pidx(a, c) : (ax & (c == 14) ? RCF::PV0 + a : (ax & (c == 15) ? RCF::PV1 + a : junk_r));
+      fp.lp1[v] = up ? a * LDS_LD + c
+                     : (ax & (c == 14) ? a * LDS_LD + 11 : (ax & (c == 15) ? a * LDS_LD + 12 : junk_l));
+      fp.lp2[v] = up ? c * LDS_LD + a : fp.lp1[v];
     }
   }
-  static MR_HD void frag_finish(int k, int lane, T delta, const T* raw, T* eb, T* hc, T& ab, T* ac) {
-    const int g = lane >> 4, c = lane & 15;
-    int idx;
-    bool data;
-    T cst;
+  static MR_HD void frag_load(const MR_GLOBAL T* Rk, const FragPlan& fp, T* raw) {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) { ehat_src(k, 4 * s + g, c, idx, data, cst); eb[s] = data ? raw[s] : cst; }
-    ehat_src(k, c, NX + g, idx, data, cst);
-    ab = ((c < NX) & (g < NU)) ? (data ? raw[4] : cst) : T(0);
+    for (int q = 0; q < 13; ++q) raw[q] = Rk[fp.off[q]];
+  }
+  static MR_HD void frag_finish(int k, const FragPlan& fp, T delta, const T* raw, T* eb, T* hc, T& ab, T* ac) {
+    const unsigned one = k > 0 ? fp.one_pos : fp.one_k0;
+    auto val = [&](int q) -> T {
+      return ((fp.data >> q) & 1u) ? raw[q] : (((one >> q) & 1u) ? T(1) : T(0));
+    };
+#pragma unroll
+    for (int s = 0; s < 4; ++s) eb[s] = val(s);
+    ab = val(4);
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      const int a = drow(g, v);
-      hc[v] = a < NZ ? raw[5 + v] + (a == c ? delta : T(0)) : T(0);
-      ehat_src(k, a, c, idx, data, cst);
-      ac[v] = ((a < NX) & ((c < NX) | (c == 14))) ? (data ? raw[9 + v] : cst) : T(0);
+      hc[v] = val(5 + v) + (((fp.dlt >> (5 + v)) & 1u) ? delta : T(0));
+      ac[v] = val(9 + v);
     }
   }
 
@@ -528,13 +557,15 @@ struct WaveSolver {
       Rn[RCF::PV1 + l] = p1;
     }
     wsync_lds(w);
+    FragPlan fp;
+    frag_plan(l, fp);
     T raw_n[13];
-    frag_load(R(N - 1), N - 1, l, raw_n);
+    frag_load(R(N - 1), fp, raw_n);
     for (int k = N - 1; k >= 0; --k) {
       MR_GLOBAL T* Rk = R(k);
       T eb[4], dq[4], dacl[4], ab;
-      frag_finish(k, l, delta, raw_n, eb, dq, ab, dacl);
-      if (k >= 1) frag_load(R(k - 1), k - 1, l, raw_n);
+      frag_finish(k, fp, delta, raw_n, eb, dq, ab, dacl);
+      if (k >= 1) frag_load(R(k - 1), fp, raw_n);
       // X = P^ E^  (A fragment s: P^[c][4s+g])
       T dx[4] = {T(0), T(0), T(0), T(0)};
 #pragma unroll
@@ -583,26 +614,12 @@ struct WaveSolver {
       const T kb = g < NU ? (c < NX ? -kg : (c == 14 ? -kf : T(0))) : T(0);
       wmfma(w, ab, kb, dacl);
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int a = drow(g, v);
+      for (int v = 0; v < 4; ++v) {  // branch-free: lanes without a target write their discard slot
         const T pv = dq[v] - dw[v];
-        if (a < NX) {
-          if (c < NX) {
-            Rk[RCF::ACL + a * NX + c] = dacl[v];
-            if (a <= c) {
-              Rk[RCF::P + pidx(a, c)] = pv;
-              LP[a * LDS_LD + c] = pv;
-              LP[c * LDS_LD + a] = pv;
-            }
-          } else if (c == 14) {
-            Rk[RCF::FF + a] = dacl[v];
-            Rk[RCF::PV0 + a] = pv;
-            LP[a * LDS_LD + 11] = pv;
-          } else if (c == 15) {
-            Rk[RCF::PV1 + a] = pv;
-            LP[a * LDS_LD + 12] = pv;
-          }
-        }
+        Rk[fp.st_a[v]] = dacl[v];
+        Rk[fp.st_p[v]] = pv;
+        LP[fp.lp1[v]] = pv;
+        LP[fp.lp2[v]] = pv;
       }
       wsync_lds(w);
     }
@@ -615,6 +632,7 @@ struct WaveSolver {
   //   i < 11 owns dx[i], the 11 values are shared with v_readlane, one 11-term dot per step.
   //   Then stage-parallel: du_k = K_k dx_k + k0 + mu k1, slack/dual steps, costates.
   MR_SWEEP void forward(T& ap, T& ad, T& gphi) {
+    const unsigned long long tf0 = trace ? MR_CLOCK() : 0ull;
     const T mu = this->mu;
     const T tau = mr_max(T(0.99), T(1) - mu);
     T dz[NZS];
@@ -628,23 +646,33 @@ struct WaveSolver {
       const int i = ln < NX ? ln : 0;
       T dxi = T(0);
       if (ln < NX) LDX[ln] = T(0);
-      T ar_n[NX], f_n;
-      for (int j = 0; j < NX; ++j) ar_n[j] = R(0)[RCF::ACL + i * NX + j];
-      f_n = R(0)[RCF::FF + i];
-      for (int k = 0; k < N; ++k) {
-        T ar[NX];
-        for (int j = 0; j < NX; ++j) ar[j] = ar_n[j];
-        const T fi = f_n;
-        if (k + 1 < N) {
-          for (int j = 0; j < NX; ++j) ar_n[j] = R(k + 1)[RCF::ACL + i * NX + j];
-          f_n = R(k + 1)[RCF::FF + i];
+      // row i of the closed-loop map and f[i], prefetched PD stages ahead (register ring)
+      constexpr int PD = 4;
+      T ar_r[PD][NX], f_r[PD];
+#pragma unroll
+      for (int d = 0; d < PD; ++d) {
+        const int kk = d < N ? d : N - 1;
+        for (int j = 0; j < NX; ++j) ar_r[d][j] = R(kk)[RCF::ACL + i * NX + j];
+        f_r[d] = R(kk)[RCF::FF + i];
+      }
+      for (int k0 = 0; k0 < N; k0 += PD) {
+#pragma unroll
+        for (int d = 0; d < PD; ++d) {
+          const int k = k0 + d;
+          if (k >= N) break;  // wave-uniform
+          T ar[NX];
+          for (int j = 0; j < NX; ++j) ar[j] = ar_r[d][j];
+          const T fi = f_r[d];
+          const int kn = k + PD < N ? k + PD : N - 1;
+          for (int j = 0; j < NX; ++j) ar_r[d][j] = R(kn)[RCF::ACL + i * NX + j];
+          f_r[d] = R(kn)[RCF::FF + i];
+          T dxv[NX];
+          wgather<T, NX>(w, dxi, dxv);
+          T acc = fi;
+          for (int j = 0; j < NX; ++j) acc += ar[j] * dxv[j];
+          dxi = ln < NX ? acc : T(0);
+          if (ln < NX) LDX[(k + 1) * 12 + ln] = dxi;
         }
-        T dxv[NX];
-        wgather<T, NX>(w, dxi, dxv);
-        T acc = fi;
-        for (int j = 0; j < NX; ++j) acc += ar[j] * dxv[j];
-        dxi = ln < NX ? acc : T(0);
-        if (ln < NX) LDX[(k + 1) * 12 + ln] = dxi;
       }
       wsync_lds(w);
       if (ln <= N)
@@ -658,6 +686,7 @@ struct WaveSolver {
         }
       }
     }
+    const unsigned long long tf1 = trace ? MR_CLOCK() : 0ull;
     // stage-parallel part
     T ap_l = T(1), ad_l = T(1), g_l = T(0);
     if (own()) {
@@ -714,6 +743,7 @@ struct WaveSolver {
     ap = wmin(w, ap_l);
     ad = wmin(w, ad_l);
     gphi = wsum(w, g_l);
+    if (trace) { tsub[0] += tf1 - tf0; tsub[1] += MR_CLOCK() - tf1; }
   }
 
   // ---------------- sweep 4: line-search trial point (writes buffer 1-cur) ----------------
@@ -912,7 +942,7 @@ struct WaveSolver {
         ftype = false;
       }
       if (!ftype) filter_add((T(1) - g_th) * th, ph - g_ph * th);
-      if (trace && ln == 0 && it < trace_cap - 1) {
+      if (trace && ln == 0 && it < trace_cap - 2) {
         double* tr = trace + 8 * it;
         tr[0] = (double)kkt; tr[1] = (double)mu; tr[2] = (double)alpha; tr[3] = (double)ad;
         tr[4] = (double)delta; tr[5] = (double)th; tr[6] = (double)ph; tr[7] = (double)(accepted ? nls : -1);
@@ -930,8 +960,10 @@ struct WaveSolver {
       double* tr = trace + 8 * (trace_cap - 1);
       for (int q = 0; q < 7; ++q) tr[q] = (double)cyc[q];
       tr[7] = (double)(trace ? MR_CLOCK() - tstart : 0ull);
+      double* tr2 = trace + 8 * (trace_cap - 2);  // sub-phases: forward seq/par, eval stage/reduce
+      for (int q = 0; q < 4; ++q) tr2[q] = (double)tsub[q];
     }
-    if (trace && ln == 0 && it < trace_cap - 1) {
+    if (trace && ln == 0 && it < trace_cap - 2) {
       double* tr = trace + 8 * it;
       tr[0] = (double)out.kkt; tr[1] = (double)fval; tr[2] = (double)theta; tr[3] = (double)stat_max;
       tr[4] = (double)pr_max; tr[5] = (double)sc; tr[6] = (double)mu; tr[7] = 1000.0 + out.status;

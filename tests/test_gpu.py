@@ -119,7 +119,10 @@ def test_c4_full_batch_fp32_properties():
         assert np.array_equal(o[k], o2[k]), k
     ok = o["status"] <= 1
     assert ok.mean() >= 0.95, np.bincount(o["status"])
-    _check_feasible(cfg, o, ok, 1e-3)
+    # acceptable points (IPOPT acceptable_tol 1e-2 of the reference's options) may violate rows by
+    # up to that tolerance; solved points (tol 1e-4) by 1e-3
+    _check_feasible(cfg, o, o["status"] == 0, 1e-3)
+    _check_feasible(cfg, o, ok, 1e-2)
     assert _defects(cfg, {k: v[..., :512] for k, v in o.items()}, ok[:512]) < 5e-3
 
 
