@@ -125,6 +125,48 @@ int mr_eval_dynamics(mr_handle* h, int32_t n, const double* x, const double* u, 
 /* workspace bytes used per instance for the handle's configuration */
 int64_t mr_workspace_bytes_per_instance(const mr_handle* h);
 
+/* ---- Centerline geometry: the per-tick MPC inputs, batched (csrc/mr_track.h) --------------------
+ * Replaces the host geometry the reference agent runs before every solve (agent.py:156-168,
+ * 271-274): splines/ParameterizedLine.py (Gx..ddGy :19-41, x_as_coeffs/y_as_coeffs :43-64,
+ * projection_local :80-97, unit_tangent/curvature/mean_curvature/unit_principal_normal :107-149)
+ * and splines/ParameterizedCenterline.py (lookup_error :61-80, error_sign :82-91).
+ * The track is built once on the host, as ParameterizedLine.from_waypoints (:162-178) does: knots
+ * t[n_t] and B-spline coefficients cx, cy[n_c] (scipy layout, k = 3), the length L, and the lane
+ * table err_left/err_right[n_rows] whose row i is s = 0.5 * i (lanes/<track>_max_error.csv).
+ * All query arrays are caller-owned DEVICE pointers of length n (outputs [m][n] component-major);
+ * calls are ordered on hip_stream.  One lane per query. */
+typedef struct mr_track mr_track;
+int mr_track_create(mr_track** tr, int32_t device, const double* t, int32_t n_t, const double* cx,
+                    const double* cy, int32_t n_c, double length, const double* err_left,
+                    const double* err_right, int32_t n_rows);
+int mr_track_destroy(mr_track* tr);
+/* out [6][n] = Gx, Gy, dGx, dGy, ddGx, ddGy at s mod L; span [n] = knot interval of G (may be NULL) */
+int mr_track_eval(const mr_track* tr, int32_t n, const double* s, double* out, int32_t* span, void* hip_stream);
+/* unit_tangent yaw, curvature, unit_principal_normal (nx, ny); mean_curvature over [s, s + mc_lookahead]
+   (N = 10) when mean_kappa != NULL; any output may be NULL */
+int mr_track_frame(const mr_track* tr, int32_t n, const double* s, double* yaw, double* kappa, double* nx,
+                   double* ny, double mc_lookahead, double* mean_kappa, void* hip_stream);
+/* error_sign(X, Y, s) -> +1 / -1 */
+int mr_track_error_sign(const mr_track* tr, int32_t n, const double* X, const double* Y, const double* s,
+                        int32_t* sign, void* hip_stream);
+/* x_as_coeffs / y_as_coeffs(s, lookahead, deg = 4): cx, cy [5][n], highest order first, global s */
+int mr_track_polyfit(const mr_track* tr, int32_t n, const double* s, const double* lookahead, double* cx,
+                     double* cy, void* hip_stream);
+/* lookup_error(s, lookahead) -> err [n] (NaN where the reference raises KeyError); row_lo / row_hi /
+   row_arg [n]: first / last / arg-min lane-table row (-1 on KeyError; each may be NULL) */
+int mr_track_lookup_error(const mr_track* tr, int32_t n, const double* s, const double* lookahead, double* err,
+                          int32_t* row_lo, int32_t* row_hi, int32_t* row_arg, void* hip_stream);
+/* projection_local(X, Y, bounds = (lo, hi)) -> s [n], dist [n]; nfev [n] may be NULL */
+int mr_track_projection(const mr_track* tr, int32_t n, const double* X, const double* Y, const double* lo,
+                        const double* hi, double* s, double* dist, int32_t* nfev, void* hip_stream);
+/* The agent's tick prep fused (agent.py:156-168 after the projection of :271-274): progress
+   s = projection_local(X, Y, (lo, hi)), cx, cy = x/y_as_coeffs(s - lookback, lookahead),
+   max_error = lookup_error(s, lookahead) - err_offset (agent.py: car_width / 2).  Outputs s, dist [n],
+   cx, cy [5][n], max_error [n]; s0 may then feed mr_solve_batch's inputs directly. */
+int mr_track_prep(const mr_track* tr, int32_t n, const double* X, const double* Y, const double* lo,
+                  const double* hi, double lookback, double lookahead, double err_offset, double* s,
+                  double* dist, double* cx, double* cy, double* max_error, void* hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -9,6 +9,8 @@
 #include <string>
 
 #include "mr_wave.h"
+#include "mr_track.h"
+#include <vector>
 
 using namespace mr;
 
@@ -80,6 +82,101 @@ __global__ void mr_eval_dynamics_kernel(ProbParams<double> P, int n, const doubl
     Dyn<double, MODEL>::f(P, x + 6 * i, u + 2 * i, f + 6 * i);
   else
     Dyn<double, MODEL>::fjh(P, x + 6 * i, u + 2 * i, nu + 6 * i, f + 6 * i, J + 48 * i, H + 36 * i);
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Centerline geometry kernels (mr_track.h): one lane per query, 256-lane workgroups.
+// ---------------------------------------------------------------------------------------------
+struct mr_track {
+  int device;
+  int nt, n_rows;
+  double L;
+  double* blob;  // device tables (track_layout)
+  TrackView view;
+};
+
+constexpr int kTrackBlock = 256;
+
+__global__ __launch_bounds__(kTrackBlock) void mr_track_eval_kernel(TrackView T, int n, const double* s, double* out,
+                                                                    int32_t* span) {
+  const int i = blockIdx.x * kTrackBlock + threadIdx.x;
+  if (i >= n) return;
+  double g[6];
+  int sp;
+  track_eval(T, s[i], g, &sp);
+  for (int c = 0; c < 6; ++c) out[(int64_t)c * n + i] = g[c];
+  if (span) span[i] = sp;
+}
+
+__global__ __launch_bounds__(kTrackBlock) void mr_track_frame_kernel(TrackView T, int n, const double* s, double* yaw,
+                                                                     double* kappa, double* nx, double* ny, double mcla,
+                                                                     double* meank) {
+  const int i = blockIdx.x * kTrackBlock + threadIdx.x;
+  if (i >= n) return;
+  double y, k, a, b;
+  track_frame(T, s[i], &y, &k, &a, &b);
+  if (yaw) yaw[i] = y;
+  if (kappa) kappa[i] = k;
+  if (nx) nx[i] = a;
+  if (ny) ny[i] = b;
+  if (meank) meank[i] = track_mean_curvature(T, s[i], mcla);
+}
+
+__global__ __launch_bounds__(kTrackBlock) void mr_track_sign_kernel(TrackView T, int n, const double* X, const double* Y,
+                                                                    const double* s, int32_t* sign) {
+  const int i = blockIdx.x * kTrackBlock + threadIdx.x;
+  if (i >= n) return;
+  sign[i] = track_error_sign(T, X[i], Y[i], s[i]);
+}
+
+__global__ __launch_bounds__(kTrackBlock) void mr_track_polyfit_kernel(TrackView T, int n, const double* s,
+                                                                       const double* la, double* cx, double* cy) {
+  const int i = blockIdx.x * kTrackBlock + threadIdx.x;
+  if (i >= n) return;
+  double a[5], b[5];
+  track_polyfit(T, s[i], la[i], a, b);
+  for (int j = 0; j < 5; ++j) { cx[(int64_t)j * n + i] = a[j]; cy[(int64_t)j * n + i] = b[j]; }
+}
+
+__global__ __launch_bounds__(kTrackBlock) void mr_track_lookup_kernel(TrackView T, int n, const double* s,
+                                                                      const double* la, double* err, int32_t* rlo,
+                                                                      int32_t* rhi, int32_t* rarg) {
+  const int i = blockIdx.x * kTrackBlock + threadIdx.x;
+  if (i >= n) return;
+  int lo, hi, arg;
+  err[i] = lane_lookup(T, s[i], la[i], &lo, &hi, &arg);
+  if (rlo) rlo[i] = lo;
+  if (rhi) rhi[i] = hi;
+  if (rarg) rarg[i] = arg;
+}
+
+__global__ __launch_bounds__(kTrackBlock) void mr_track_projection_kernel(TrackView T, int n, const double* X,
+                                                                          const double* Y, const double* lo,
+                                                                          const double* hi, double* s, double* dist,
+                                                                          int32_t* nfev) {
+  const int i = blockIdx.x * kTrackBlock + threadIdx.x;
+  if (i >= n) return;
+  int nf;
+  const double x = brent_projection(T, X[i], Y[i], lo[i], hi[i], &nf);
+  s[i] = x;
+  dist[i] = track_dist(T, x, X[i], Y[i]);
+  if (nfev) nfev[i] = nf;
+}
+
+__global__ __launch_bounds__(kTrackBlock) void mr_track_prep_kernel(TrackView T, int n, const double* X, const double* Y,
+                                                                    const double* lo, const double* hi, double lookback,
+                                                                    double lookahead, double err_offset, double* s,
+                                                                    double* dist, double* cx, double* cy, double* merr) {
+  const int i = blockIdx.x * kTrackBlock + threadIdx.x;
+  if (i >= n) return;
+  const double p = brent_projection(T, X[i], Y[i], lo[i], hi[i], nullptr);
+  s[i] = p;
+  dist[i] = track_dist(T, p, X[i], Y[i]);
+  double a[5], b[5];
+  track_polyfit(T, p - lookback, lookahead, a, b);
+  for (int j = 0; j < 5; ++j) { cx[(int64_t)j * n + i] = a[j]; cy[(int64_t)j * n + i] = b[j]; }
+  merr[i] = lane_lookup(T, p, lookahead, nullptr, nullptr, nullptr) - err_offset;
 }
 
 extern "C" {
@@ -170,6 +267,95 @@ int mr_solve_batch(mr_handle* h, int32_t B, const mr_inputs* in, mr_outputs* out
   hipStream_t st = (hipStream_t)hip_stream;
   if (h->cfg.precision == MR_PREC_FP64) return dispatch_model<double>(h, B, in, out, st);
   return dispatch_model<float>(h, B, in, out, st);
+}
+
+
+int mr_track_create(mr_track** out, int32_t device, const double* t, int32_t n_t, const double* cx, const double* cy,
+                    int32_t n_c, double length, const double* err_left, const double* err_right, int32_t n_rows) {
+  if (!out || !t || !cx || !cy || !err_left || !err_right) return fail(MR_ERR_ARG, "null argument");
+  if (n_t < 8 || n_c < 4 || n_c > n_t || n_rows < 1 || !(length > 0)) return fail(MR_ERR_ARG, "bad track sizes");
+  for (int i = 1; i < n_t; ++i)
+    if (!(t[i] >= t[i - 1])) return fail(MR_ERR_ARG, "knots not sorted");
+  const TrackLayout Lay = track_layout(n_t, n_rows);
+  std::vector<double> blob(Lay.total);
+  track_tables(t, n_t, cx, cy, n_c, err_left, err_right, n_rows, blob.data());
+  HIP_TRY(hipSetDevice(device));
+  mr_track* tr = new mr_track();
+  tr->device = device;
+  tr->nt = n_t;
+  tr->n_rows = n_rows;
+  tr->L = length;
+  hipError_t e = hipMalloc(&tr->blob, sizeof(double) * blob.size());
+  if (e == hipSuccess) e = hipMemcpy(tr->blob, blob.data(), sizeof(double) * blob.size(), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    if (tr->blob) (void)hipFree(tr->blob);
+    delete tr;
+    return fail(MR_ERR_HIP, std::string("track tables: ") + hipGetErrorString(e));
+  }
+  tr->view = track_view(tr->blob, n_t, length, n_rows);
+  *out = tr;
+  return MR_OK;
+}
+
+int mr_track_destroy(mr_track* tr) {
+  if (!tr) return MR_OK;
+  if (tr->blob) (void)hipFree(tr->blob);
+  delete tr;
+  return MR_OK;
+}
+
+#define MR_TRACK_LAUNCH(kernel, ...)                                                             \
+  do {                                                                                           \
+    if (!tr) return fail(MR_ERR_ARG, "null track");                                              \
+    if (n < 0) return fail(MR_ERR_ARG, "n < 0");                                                 \
+    if (n == 0) return MR_OK;                                                                    \
+    HIP_TRY(hipSetDevice(tr->device));                                                           \
+    hipLaunchKernelGGL(kernel, dim3((n + kTrackBlock - 1) / kTrackBlock), dim3(kTrackBlock), 0,  \
+                       (hipStream_t)hip_stream, tr->view, n, __VA_ARGS__);                       \
+    HIP_TRY(hipGetLastError());                                                                  \
+    return MR_OK;                                                                                \
+  } while (0)
+
+int mr_track_eval(const mr_track* tr, int32_t n, const double* s, double* out, int32_t* span, void* hip_stream) {
+  if (!s || !out) return fail(MR_ERR_ARG, "null argument");
+  MR_TRACK_LAUNCH(mr_track_eval_kernel, s, out, span);
+}
+
+int mr_track_frame(const mr_track* tr, int32_t n, const double* s, double* yaw, double* kappa, double* nx, double* ny,
+                   double mc_lookahead, double* mean_kappa, void* hip_stream) {
+  if (!s) return fail(MR_ERR_ARG, "null argument");
+  MR_TRACK_LAUNCH(mr_track_frame_kernel, s, yaw, kappa, nx, ny, mc_lookahead, mean_kappa);
+}
+
+int mr_track_error_sign(const mr_track* tr, int32_t n, const double* X, const double* Y, const double* s,
+                        int32_t* sign, void* hip_stream) {
+  if (!X || !Y || !s || !sign) return fail(MR_ERR_ARG, "null argument");
+  MR_TRACK_LAUNCH(mr_track_sign_kernel, X, Y, s, sign);
+}
+
+int mr_track_polyfit(const mr_track* tr, int32_t n, const double* s, const double* lookahead, double* cx, double* cy,
+                     void* hip_stream) {
+  if (!s || !lookahead || !cx || !cy) return fail(MR_ERR_ARG, "null argument");
+  MR_TRACK_LAUNCH(mr_track_polyfit_kernel, s, lookahead, cx, cy);
+}
+
+int mr_track_lookup_error(const mr_track* tr, int32_t n, const double* s, const double* lookahead, double* err,
+                          int32_t* row_lo, int32_t* row_hi, int32_t* row_arg, void* hip_stream) {
+  if (!s || !lookahead || !err) return fail(MR_ERR_ARG, "null argument");
+  MR_TRACK_LAUNCH(mr_track_lookup_kernel, s, lookahead, err, row_lo, row_hi, row_arg);
+}
+
+int mr_track_projection(const mr_track* tr, int32_t n, const double* X, const double* Y, const double* lo,
+                        const double* hi, double* s, double* dist, int32_t* nfev, void* hip_stream) {
+  if (!X || !Y || !lo || !hi || !s || !dist) return fail(MR_ERR_ARG, "null argument");
+  MR_TRACK_LAUNCH(mr_track_projection_kernel, X, Y, lo, hi, s, dist, nfev);
+}
+
+int mr_track_prep(const mr_track* tr, int32_t n, const double* X, const double* Y, const double* lo, const double* hi,
+                  double lookback, double lookahead, double err_offset, double* s, double* dist, double* cx,
+                  double* cy, double* max_error, void* hip_stream) {
+  if (!X || !Y || !lo || !hi || !s || !dist || !cx || !cy || !max_error) return fail(MR_ERR_ARG, "null argument");
+  MR_TRACK_LAUNCH(mr_track_prep_kernel, X, Y, lo, hi, lookback, lookahead, err_offset, s, dist, cx, cy, max_error);
 }
 
 }  // extern "C"

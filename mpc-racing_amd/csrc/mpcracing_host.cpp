@@ -9,6 +9,7 @@
 #include <string.h>
 #include <vector>
 #include "mr_wave.h"
+#include "mr_track.h"
 
 using namespace mr;
 
@@ -89,6 +90,65 @@ int mrh_eval_dynamics(const mr_config* c, const double* a_front, double Fz_front
     case MR_MODEL_BLENDED_PACEJKA: Dyn<double, MODEL_BLEND_PACEJKA>::fjh(P, x, u, nu, f, J, H); break;
     case MR_MODEL_DYNAMIC_PACEJKA: Dyn<double, MODEL_DYN_PACEJKA>::fjh(P, x, u, nu, f, J, H); break;
     default: return -1;
+  }
+  return 0;
+}
+
+// ---- centerline geometry (mr_track.h) on host arrays: the same functions as the gfx950 kernels ----
+int mrh_track_blob_size(int nt, int n_rows) { return track_layout(nt, n_rows).total; }
+int mrh_track_build(const double* t, int nt, const double* cx, const double* cy, int nc, const double* el,
+                    const double* er, int n_rows, double* blob) {
+  track_tables(t, nt, cx, cy, nc, el, er, n_rows, blob);
+  return 0;
+}
+int mrh_track_eval(const double* blob, int nt, double L, int n_rows, int n, const double* s, double* out, int* span) {
+  TrackView T = track_view(blob, nt, L, n_rows);
+  for (int i = 0; i < n; ++i) {
+    double g[6];
+    int sp;
+    track_eval(T, s[i], g, &sp);
+    for (int c = 0; c < 6; ++c) out[(int64_t)c * n + i] = g[c];
+    if (span) span[i] = sp;
+  }
+  return 0;
+}
+int mrh_track_frame(const double* blob, int nt, double L, int n_rows, int n, const double* s, double* yaw,
+                    double* kappa, double* nx, double* ny, double mcla, double* meank) {
+  TrackView T = track_view(blob, nt, L, n_rows);
+  for (int i = 0; i < n; ++i) {
+    track_frame(T, s[i], yaw + i, kappa + i, nx + i, ny + i);
+    if (meank) meank[i] = track_mean_curvature(T, s[i], mcla);
+  }
+  return 0;
+}
+int mrh_track_sign(const double* blob, int nt, double L, int n_rows, int n, const double* X, const double* Y,
+                   const double* s, int* sign) {
+  TrackView T = track_view(blob, nt, L, n_rows);
+  for (int i = 0; i < n; ++i) sign[i] = track_error_sign(T, X[i], Y[i], s[i]);
+  return 0;
+}
+int mrh_track_polyfit(const double* blob, int nt, double L, int n_rows, int n, const double* s, const double* la,
+                      double* cx, double* cy) {
+  TrackView T = track_view(blob, nt, L, n_rows);
+  for (int i = 0; i < n; ++i) {
+    double a[5], b[5];
+    track_polyfit(T, s[i], la[i], a, b);
+    for (int j = 0; j < 5; ++j) { cx[(int64_t)j * n + i] = a[j]; cy[(int64_t)j * n + i] = b[j]; }
+  }
+  return 0;
+}
+int mrh_track_lookup(const double* blob, int nt, double L, int n_rows, int n, const double* s, const double* la,
+                     double* err, int* lo, int* hi, int* arg) {
+  TrackView T = track_view(blob, nt, L, n_rows);
+  for (int i = 0; i < n; ++i) err[i] = lane_lookup(T, s[i], la[i], lo + i, hi + i, arg + i);
+  return 0;
+}
+int mrh_track_projection(const double* blob, int nt, double L, int n_rows, int n, const double* X, const double* Y,
+                         const double* lo, const double* hi, double* s, double* dist, int* nfev) {
+  TrackView T = track_view(blob, nt, L, n_rows);
+  for (int i = 0; i < n; ++i) {
+    s[i] = brent_projection(T, X[i], Y[i], lo[i], hi[i], nfev + i);
+    dist[i] = track_dist(T, s[i], X[i], Y[i]);
   }
   return 0;
 }

@@ -1,0 +1,391 @@
+// Centerline geometry on the device: the per-tick MPC inputs of the reference agent
+// (agent.py:156-168, 271-274) for a batch of queries, one lane per query.
+//
+//   K5  cubic B-spline evaluation G, G', G''   splines/ParameterizedLine.py:19-41 (scipy BSpline:
+//                                               interval search + de Boor; derivative splines by splder)
+//   K6  x_as_coeffs / y_as_coeffs (deg 4)      splines/ParameterizedLine.py:43-64 (np.polyfit)
+//   K7  lookup_error (lane-table window min)   splines/ParameterizedCenterline.py:61-80
+//   K8  projection_local (bounded Brent)       splines/ParameterizedLine.py:80-97 (scipy
+//                                               _minimize_scalar_bounded, xatol 1e-5, maxiter 500)
+//   A15 tangent yaw, curvature, mean curvature, principal normal, error sign
+//                                               ParameterizedLine.py:107-149, ParameterizedCenterline.py:82-91
+//
+// Operations follow the order the reference's libraries execute them (IEEE fp64, built without
+// FP contraction), so knot-span indices, lane-table rows, spline values and the Brent step
+// sequence reproduce the reference bit for bit.  The quartic fit solves the same least-squares
+// problem in a centred, scaled variable (numpy's LAPACK SVD is not reproducible bit for bit);
+// its parity is stated on the fitted values.
+#pragma once
+#include "mr_common.h"
+
+namespace mr {
+
+// One scipy-layout B-spline (t, c, k), extrapolate=True.
+struct SplineView {
+  const double* t;
+  const double* c;
+  int nt, k;
+};
+
+// Centerline tables of one track (built once on the host, see track_tables()).
+struct TrackView {
+  SplineView x[3], y[3];  // G, G', G'' (k = 3, 2, 1)
+  double L;               // track length: queries are taken modulo L (ParameterizedLine.py:19-25)
+  const double* err_left;  // lane table, row i at s = 0.5 * i (lanes/<track>_max_error.csv)
+  const double* err_right;
+  int n_rows;
+};
+
+// CPython float_rem (the result takes the sign of the divisor)
+MR_HD double py_mod(double x, double y) {
+  double m = fmod(x, y);
+  if (m != 0.0) {
+    if ((y < 0) != (m < 0)) m += y;
+  } else {
+    m = copysign(0.0, y);
+  }
+  return m;
+}
+
+// Python round(x) on floats: half to even (rint in the default rounding mode)
+MR_HD double py_round(double x) { return rint(x); }
+
+// scipy _find_interval: largest l in [k, n-1] with t[l] <= x (k when none or NaN)
+MR_HD int spline_span(const SplineView& s, double x) {
+  const int k = s.k, n = s.nt - k - 1;
+  int lo = k, hi = n - 1;  // predicate x >= t[l] is monotone in l
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (x >= s.t[mid]) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+// de Boor basis (scipy _deBoor_D, m = 0) and the coefficient sum, in scipy's order
+MR_HD double spline_eval(const SplineView& s, double x, int* span_out = nullptr) {
+  const int k = s.k;
+  const int ell = spline_span(s, x);
+  if (span_out) *span_out = ell;
+  double h[4] = {1.0, 0.0, 0.0, 0.0}, hh[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int j = 1; j <= k; ++j) {
+    for (int q = 0; q < j; ++q) hh[q] = h[q];
+    h[0] = 0.0;
+    for (int n = 1; n <= j; ++n) {
+      const int ind = ell + n;
+      const double xb = s.t[ind], xa = s.t[ind - j];
+      if (xb == xa) {
+        h[n] = 0.0;
+        continue;
+      }
+      const double w = hh[n - 1] / (xb - xa);
+      h[n - 1] += w * (xb - x);
+      h[n] = w * (x - xa);
+    }
+  }
+  double acc = 0.0;
+  for (int a = 0; a <= k; ++a) acc += s.c[ell + a - k] * h[a];
+  return acc;
+}
+
+// Gx, Gy, dGx, dGy, ddGx, ddGy at s mod L; span = knot interval of G
+MR_HD void track_eval(const TrackView& T, double s, double* out6, int* span) {
+  const double m = py_mod(s, T.L);
+  out6[0] = spline_eval(T.x[0], m, span);
+  out6[1] = spline_eval(T.y[0], m);
+  out6[2] = spline_eval(T.x[1], m);
+  out6[3] = spline_eval(T.y[1], m);
+  out6[4] = spline_eval(T.x[2], m);
+  out6[5] = spline_eval(T.y[2], m);
+}
+
+// dist(s) = sqrt((Gx(s) - X)**2 + (Gy(s) - Y)**2)  (ParameterizedLine.py:95)
+MR_HD double track_dist(const TrackView& T, double s, double X, double Y) {
+  const double m = py_mod(s, T.L);
+  const double dx = spline_eval(T.x[0], m) - X, dy = spline_eval(T.y[0], m) - Y;
+  return sqrt(dx * dx + dy * dy);
+}
+
+// scipy.optimize._minimize_scalar_bounded, step for step; returns the minimiser
+MR_HD double brent_projection(const TrackView& T, double X, double Y, double x1, double x2, int* nfev) {
+  const double xatol = 1e-5;
+  const int maxiter = 500;
+  const double sqrt_eps = 1.4832396974191326e-08;  // math.sqrt(2.2e-16)
+  const double golden_mean = 0.3819660112501051;   // 0.5 * (3.0 - math.sqrt(5.0))
+  double a = x1, b = x2;
+  double fulc = a + golden_mean * (b - a);
+  double nfc = fulc, xf = fulc;
+  double rat = 0.0, e = 0.0;
+  double fx = track_dist(T, xf, X, Y);
+  int num = 1;
+  double ffulc = fx, fnfc = fx;
+  double xm = 0.5 * (a + b);
+  double tol1 = sqrt_eps * fabs(xf) + xatol / 3.0;
+  double tol2 = 2.0 * tol1;
+  while (fabs(xf - xm) > (tol2 - 0.5 * (b - a))) {
+    bool golden = true;
+    if (fabs(e) > tol1) {
+      golden = false;
+      double r = (xf - nfc) * (fx - ffulc);
+      double q = (xf - fulc) * (fx - fnfc);
+      double p = (xf - fulc) * q - (xf - nfc) * r;
+      q = 2.0 * (q - r);
+      if (q > 0.0) p = -p;
+      q = fabs(q);
+      r = e;
+      e = rat;
+      if (fabs(p) < fabs(0.5 * q * r) && p > q * (a - xf) && p < q * (b - xf)) {
+        rat = (p + 0.0) / q;
+        const double x = xf + rat;
+        if ((x - a) < tol2 || (b - x) < tol2) {
+          const double d = xm - xf;
+          const double si = (d > 0 ? 1.0 : (d < 0 ? -1.0 : 0.0)) + (xm == xf ? 1.0 : 0.0);
+          rat = tol1 * si;
+        }
+      } else {
+        golden = true;
+      }
+    }
+    if (golden) {
+      e = (xf >= xm) ? (a - xf) : (b - xf);
+      rat = golden_mean * e;
+    }
+    const double si = (rat > 0 ? 1.0 : (rat < 0 ? -1.0 : 0.0)) + (rat == 0 ? 1.0 : 0.0);
+    const double x = xf + si * (fabs(rat) > tol1 ? fabs(rat) : tol1);
+    const double fu = track_dist(T, x, X, Y);
+    num += 1;
+    if (fu <= fx) {
+      if (x >= xf) a = xf;
+      else b = xf;
+      fulc = nfc; ffulc = fnfc;
+      nfc = xf; fnfc = fx;
+      xf = x; fx = fu;
+    } else {
+      if (x < xf) a = x;
+      else b = x;
+      if (fu <= fnfc || nfc == xf) {
+        fulc = nfc; ffulc = fnfc;
+        nfc = x; fnfc = fu;
+      } else if (fu <= ffulc || fulc == xf || fulc == nfc) {
+        fulc = x; ffulc = fu;
+      }
+    }
+    xm = 0.5 * (a + b);
+    tol1 = sqrt_eps * fabs(xf) + xatol / 3.0;
+    tol2 = 2.0 * tol1;
+    if (num >= maxiter) break;
+  }
+  if (nfev) *nfev = num;
+  return xf;
+}
+
+// lookup_error: min over the 0.5 m rows of [s, s + lookahead) of min(left, right); rows keyed
+// by round-half-even(2 (q mod L)) / 2.  NaN when a key is outside the table (the reference's
+// KeyError); row_lo / row_hi / row_arg = first, last, arg-min row (-1 then).
+MR_HD double lane_lookup(const TrackView& T, double s, double lookahead, int* row_lo, int* row_hi, int* row_arg) {
+  const double s_round = py_round(s * 2) / 2;
+  const double la = py_round(lookahead * 2) / 2;
+  const double stop = s + la;
+  const double span = ceil((stop - s_round) / 0.5);  // numpy.arange length
+  const int n = span > 0 ? (int)span : 0;
+  double left_min = 10000, right_min = 10000;
+  int arg_left = -1, arg_right = -1, lo = -1, hi = -1;
+  for (int i = 0; i < n; ++i) {
+    const double q = s_round + i * 0.5;
+    const double key = py_round(py_mod(q, T.L) * 2) / 2;
+    const int row = (int)(key * 2);
+    if (row < 0 || row >= T.n_rows) {
+      if (row_lo) *row_lo = -1;
+      if (row_hi) *row_hi = -1;
+      if (row_arg) *row_arg = -1;
+      return NAN;
+    }
+    if (i == 0) lo = row;
+    hi = row;
+    const double left = T.err_left[row], right = T.err_right[row];
+    if (left < left_min) { left_min = left; arg_left = row; }
+    if (right < right_min) { right_min = right; arg_right = row; }
+  }
+  if (row_lo) *row_lo = lo;
+  if (row_hi) *row_hi = hi;
+  const bool take_left = left_min < right_min;  // Python min(right_min, left_min)
+  if (row_arg) *row_arg = take_left ? arg_left : arg_right;
+  return take_left ? left_min : right_min;
+}
+
+// unit_tangent yaw, curvature |x'y'' - y'x''|, unit principal normal (t_y, -t_x)
+MR_HD void track_frame(const TrackView& T, double s, double* yaw, double* kappa, double* nx, double* ny) {
+  double g[6];
+  track_eval(T, s, g, nullptr);
+  const double nrm = sqrt(g[2] * g[2] + g[3] * g[3]);
+  const double ux = g[2] / nrm, uy = g[3] / nrm;
+  *yaw = atan2(uy, ux);
+  *kappa = fabs(g[2] * g[5] - g[3] * g[4]);
+  *nx = uy;
+  *ny = -ux;
+}
+
+// mean_curvature(s, lookahead, N=10): (1/N) * sum of curvature on linspace(s, s + lookahead, N)
+MR_HD double track_mean_curvature(const TrackView& T, double s, double lookahead) {
+  const int NS = 10;
+  const double stop = s + lookahead;
+  const double step = (stop - s) / (NS - 1);
+  double sum = 0.0;
+  for (int i = 0; i < NS; ++i) {
+    const double q = i == NS - 1 ? stop : i * step + s;
+    double g[6];
+    track_eval(T, q, g, nullptr);
+    sum += fabs(g[2] * g[5] - g[3] * g[4]);
+  }
+  return (1.0 / NS) * sum;
+}
+
+// error_sign: +1 if |d - n| < |d + n| else -1, d = (X - Gx, Y - Gy), n the principal normal
+MR_HD int track_error_sign(const TrackView& T, double X, double Y, double s) {
+  double g[6], yaw, kappa, nx, ny;
+  track_eval(T, s, g, nullptr);
+  track_frame(T, s, &yaw, &kappa, &nx, &ny);
+  const double dx = X - g[0], dy = Y - g[1];
+  const double a = sqrt((dx - nx) * (dx - nx) + (dy - ny) * (dy - ny));
+  const double b = sqrt((dx + nx) * (dx + nx) + (dy + ny) * (dy + ny));
+  return a < b ? 1 : -1;
+}
+
+// x_as_coeffs / y_as_coeffs(s, lookahead, deg=4): least-squares quartic through the 50 samples of
+// G on numpy.linspace(0, lookahead, 50) + s, in GLOBAL s, highest order first (np.polyfit).
+// Normal equations in u = (s' - mid) / h (moments of a well-conditioned basis), Cholesky 5x5,
+// then the exact binomial expansion back to powers of s'.
+MR_HD void track_polyfit(const TrackView& T, double s, double lookahead, double* cx, double* cy) {
+  const int M = 50;
+  const double h = lookahead > 0 ? 0.5 * lookahead : 1.0;
+  const double mid = s + 0.5 * lookahead;
+  const double step = lookahead / (M - 1);
+  double mom[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, rx[5] = {0, 0, 0, 0, 0}, ry[5] = {0, 0, 0, 0, 0};
+  for (int i = 0; i < M; ++i) {
+    const double q = (i == M - 1 ? lookahead : i * step) + s;
+    const double m = py_mod(q, T.L);
+    const double yx = spline_eval(T.x[0], m), yy = spline_eval(T.y[0], m);
+    const double u = (q - mid) / h;
+    double p = 1.0;
+    for (int j = 0; j < 9; ++j) {
+      mom[j] += p;
+      if (j < 5) { rx[j] += p * yx; ry[j] += p * yy; }
+      p *= u;
+    }
+  }
+  double G[5][5], L[5][5];
+  for (int i = 0; i < 5; ++i)
+    for (int j = 0; j < 5; ++j) { G[i][j] = mom[i + j]; L[i][j] = 0.0; }
+  for (int j = 0; j < 5; ++j) {
+    double d = G[j][j];
+    for (int q = 0; q < j; ++q) d -= L[j][q] * L[j][q];
+    L[j][j] = sqrt(d);
+    for (int i = j + 1; i < 5; ++i) {
+      double v = G[i][j];
+      for (int q = 0; q < j; ++q) v -= L[i][q] * L[j][q];
+      L[i][j] = v / L[j][j];
+    }
+  }
+  double ax[5], ay[5];
+  for (int i = 0; i < 5; ++i) {  // L y = r
+    double vx = rx[i], vy = ry[i];
+    for (int q = 0; q < i; ++q) { vx -= L[i][q] * ax[q]; vy -= L[i][q] * ay[q]; }
+    ax[i] = vx / L[i][i];
+    ay[i] = vy / L[i][i];
+  }
+  for (int i = 4; i >= 0; --i) {  // L^T a = y
+    double vx = ax[i], vy = ay[i];
+    for (int q = i + 1; q < 5; ++q) { vx -= L[q][i] * ax[q]; vy -= L[q][i] * ay[q]; }
+    ax[i] = vx / L[i][i];
+    ay[i] = vy / L[i][i];
+  }
+  // sum_j a_j ((s' - mid) / h)^j  ->  ascending powers of s'
+  const double binom[5][5] = {{1, 0, 0, 0, 0}, {1, 1, 0, 0, 0}, {1, 2, 1, 0, 0}, {1, 3, 3, 1, 0}, {1, 4, 6, 4, 1}};
+  double gx[5] = {0, 0, 0, 0, 0}, gy[5] = {0, 0, 0, 0, 0};
+  double hj = 1.0;
+  for (int j = 0; j < 5; ++j) {
+    const double sx = ax[j] / hj, sy = ay[j] / hj;
+    for (int i = 0; i <= j; ++i) {
+      double pm = 1.0;
+      for (int q = 0; q < j - i; ++q) pm *= -mid;
+      gx[i] += sx * binom[j][i] * pm;
+      gy[i] += sy * binom[j][i] * pm;
+    }
+    hj *= h;
+  }
+  for (int j = 0; j < 5; ++j) {
+    cx[j] = gx[4 - j];
+    cy[j] = gy[4 - j];
+  }
+}
+
+// Host: the device tables of one track from the scipy spline (t, c, k = 3): G's coefficients
+// padded to len(t), then splder's rule twice, exactly as scipy BSpline.derivative() computes it
+// (the reference rebuilds the derivative spline on every call, ParameterizedLine.py:27-41).
+// Blob layout: t | cx | cy | t1 | dcx | dcy | t2 | ddcx | ddcy | err_left | err_right.
+struct TrackLayout {
+  int nt, off_t, off_cx, off_cy, off_t1, off_dcx, off_dcy, off_t2, off_ddcx, off_ddcy, off_el, off_er, total;
+};
+inline TrackLayout track_layout(int nt, int n_rows) {
+  TrackLayout L;
+  L.nt = nt;
+  int o = 0;
+  L.off_t = o; o += nt;
+  L.off_cx = o; o += nt;
+  L.off_cy = o; o += nt;
+  L.off_t1 = o; o += nt - 2;
+  L.off_dcx = o; o += nt - 2;
+  L.off_dcy = o; o += nt - 2;
+  L.off_t2 = o; o += nt - 4;
+  L.off_ddcx = o; o += nt - 4;
+  L.off_ddcy = o; o += nt - 4;
+  L.off_el = o; o += n_rows;
+  L.off_er = o; o += n_rows;
+  L.total = o;
+  return L;
+}
+// splder on (t, c[len(t)], k): returns c' of length len(t) - 2 (knots t[1:-1], degree k - 1)
+inline void splder_coeffs(const double* t, const double* c, int nt, int k, double* out) {
+  const int m = nt - k - 2;  // len(dt)
+  for (int i = 0; i < m; ++i) {
+    const double dt = t[i + k + 1] - t[i + 1];
+    out[i] = ((c[i + 1] - c[i]) * (double)k) / dt;
+  }
+  for (int i = m; i < nt - 2; ++i) out[i] = 0.0;
+}
+inline void track_tables(const double* t, int nt, const double* cx, const double* cy, int nc, const double* el,
+                         const double* er, int n_rows, double* blob) {
+  const TrackLayout L = track_layout(nt, n_rows);
+  for (int i = 0; i < nt; ++i) {
+    blob[L.off_t + i] = t[i];
+    blob[L.off_cx + i] = i < nc ? cx[i] : 0.0;
+    blob[L.off_cy + i] = i < nc ? cy[i] : 0.0;
+  }
+  for (int i = 0; i < nt - 2; ++i) blob[L.off_t1 + i] = t[i + 1];
+  splder_coeffs(blob + L.off_t, blob + L.off_cx, nt, 3, blob + L.off_dcx);
+  splder_coeffs(blob + L.off_t, blob + L.off_cy, nt, 3, blob + L.off_dcy);
+  for (int i = 0; i < nt - 4; ++i) blob[L.off_t2 + i] = t[i + 2];
+  splder_coeffs(blob + L.off_t1, blob + L.off_dcx, nt - 2, 2, blob + L.off_ddcx);
+  splder_coeffs(blob + L.off_t1, blob + L.off_dcy, nt - 2, 2, blob + L.off_ddcy);
+  for (int i = 0; i < n_rows; ++i) {
+    blob[L.off_el + i] = el[i];
+    blob[L.off_er + i] = er[i];
+  }
+}
+inline TrackView track_view(const double* blob, int nt, double length, int n_rows) {
+  const TrackLayout L = track_layout(nt, n_rows);
+  TrackView T;
+  T.x[0] = {blob + L.off_t, blob + L.off_cx, nt, 3};
+  T.y[0] = {blob + L.off_t, blob + L.off_cy, nt, 3};
+  T.x[1] = {blob + L.off_t1, blob + L.off_dcx, nt - 2, 2};
+  T.y[1] = {blob + L.off_t1, blob + L.off_dcy, nt - 2, 2};
+  T.x[2] = {blob + L.off_t2, blob + L.off_ddcx, nt - 4, 1};
+  T.y[2] = {blob + L.off_t2, blob + L.off_ddcy, nt - 4, 1};
+  T.L = length;
+  T.err_left = blob + L.off_el;
+  T.err_right = blob + L.off_er;
+  T.n_rows = n_rows;
+  return T;
+}
+
+}  // namespace mr

@@ -499,10 +499,10 @@ struct WaveSolver {
       // outputs of D register v: closed-loop map, packed-upper P | p0 | p1, LDS image of P^
       const int junk_r = RCF::JUNK + lane, junk_l = LJUNK_OFF - LP_OFF + lane;  // lp* index from LP
       const bool ax = a < NX, up = ax & (c < NX) & (a <= c);
-      fp.st_a[v] = ax & (c < NX) ? RCF::ACL + a * NX + c : (ax & (c == 14) ? RCF::FF + a : junk_r);
-      fp.st_p[v] = up ? RCF::P + pidx(a, c) : (ax & (c == 14) ? RCF::PV0 + a : (ax & (c == 15) ? RCF::PV1 + a : junk_r));
-      fp.lp1[v] = up ? a * LDS_LD + c
-                     : (ax & (c == 14) ? a * LDS_LD + 11 : (ax & (c == 15) ? a * LDS_LD + 12 : junk_l));
+      const bool c14 = ax & (c == 14), c15 = ax & (c == 15);
+      fp.st_a[v] = (ax & (c < NX)) ? RCF::ACL + a * NX + c : (c14 ? RCF::FF + a : junk_r);
+      fp.st_p[v] = up ? RCF::P + pidx(a, c) : (c14 ? RCF::PV0 + a : (c15 ? RCF::PV1 + a : junk_r));
+      fp.lp1[v] = up ? a * LDS_LD + c : (c14 ? a * LDS_LD + 11 : (c15 ? a * LDS_LD + 12 : junk_l));
       fp.lp2[v] = up ? c * LDS_LD + a : fp.lp1[v];
     }
   }

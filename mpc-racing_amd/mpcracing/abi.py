@@ -40,7 +40,9 @@ class MROutputs(ctypes.Structure):
 
 # every symbol declared in include/mpcracing.h (checked by tests/test_abi.py)
 EXPORTS = ["mr_version", "mr_last_error", "mr_config_default", "mr_create", "mr_destroy", "mr_set_tyres",
-           "mr_solve_batch", "mr_workspace_bytes_per_instance", "mr_eval_dynamics"]
+           "mr_solve_batch", "mr_workspace_bytes_per_instance", "mr_eval_dynamics",
+           "mr_track_create", "mr_track_destroy", "mr_track_eval", "mr_track_frame", "mr_track_error_sign",
+           "mr_track_polyfit", "mr_track_lookup_error", "mr_track_projection", "mr_track_prep"]
 
 
 def _bind_product(lib):
@@ -55,6 +57,16 @@ def _bind_product(lib):
     lib.mr_eval_dynamics.argtypes = [ctypes.c_void_p, _I32] + [ctypes.c_void_p] * 7
     lib.mr_workspace_bytes_per_instance.argtypes = [ctypes.c_void_p]
     lib.mr_workspace_bytes_per_instance.restype = ctypes.c_int64
+    V = ctypes.c_void_p
+    lib.mr_track_create.argtypes = [ctypes.POINTER(V), _I32, _PD, _I32, _PD, _PD, _I32, _D, _PD, _PD, _I32]
+    lib.mr_track_destroy.argtypes = [V]
+    lib.mr_track_eval.argtypes = [V, _I32, V, V, V, V]
+    lib.mr_track_frame.argtypes = [V, _I32, V, V, V, V, V, _D, V, V]
+    lib.mr_track_error_sign.argtypes = [V, _I32, V, V, V, V, V]
+    lib.mr_track_polyfit.argtypes = [V, _I32, V, V, V, V, V]
+    lib.mr_track_lookup_error.argtypes = [V, _I32, V, V, V, V, V, V, V]
+    lib.mr_track_projection.argtypes = [V, _I32, V, V, V, V, V, V, V, V]
+    lib.mr_track_prep.argtypes = [V, _I32, V, V, V, V, _D, _D, _D, V, V, V, V, V, V]
     return lib
 
 
@@ -79,4 +91,13 @@ def load_host_twin(path=HOST_TWIN_LIB):
                                     ctypes.POINTER(MRInputs), ctypes.POINTER(MROutputs), ctypes.c_int]
     lib.mrh_eval_dynamics.argtypes = [ctypes.POINTER(MRConfig), _PD, _D, _PD, _D, _PD, _PD, _PD, _PD, _PD, _PD]
     lib.mrh_pacejka.argtypes = [_PD, _D, _D, ctypes.c_int, _PD]
+    V, I = ctypes.c_void_p, ctypes.c_int
+    lib.mrh_track_blob_size.argtypes = [I, I]
+    lib.mrh_track_build.argtypes = [V, I, V, V, I, V, V, I, V]
+    lib.mrh_track_eval.argtypes = [V, I, _D, I, I, V, V, V]
+    lib.mrh_track_frame.argtypes = [V, I, _D, I, I, V, V, V, V, V, _D, V]
+    lib.mrh_track_sign.argtypes = [V, I, _D, I, I, V, V, V, V]
+    lib.mrh_track_polyfit.argtypes = [V, I, _D, I, I, V, V, V, V]
+    lib.mrh_track_lookup.argtypes = [V, I, _D, I, I, V, V, V, V, V, V]
+    lib.mrh_track_projection.argtypes = [V, I, _D, I, I, V, V, V, V, V, V, V]
     return lib

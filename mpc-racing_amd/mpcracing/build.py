@@ -9,7 +9,7 @@ import subprocess
 from .abi import CSRC, PRODUCT_LIB, HOST_TWIN_LIB
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-SOURCES = ["mpcracing.hip", "mr_batch.h", "mr_solver.h", "mr_common.h", "gen_dynamics.h", "mr_wave.h", "mr_wave_prims.h"]
+SOURCES = ["mpcracing.hip", "mr_batch.h", "mr_solver.h", "mr_common.h", "gen_dynamics.h", "mr_wave.h", "mr_wave_prims.h", "mr_track.h"]
 INCLUDE = os.path.abspath(os.path.join(CSRC, "..", "..", "include"))
 
 
@@ -42,7 +42,7 @@ def build_host_twin(force=False, verbose=True):
            [os.path.join(INCLUDE, "mpcracing.h")]
     if not force and not _stale(HOST_TWIN_LIB, deps):
         return HOST_TWIN_LIB
-    cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-o", HOST_TWIN_LIB,
+    cmd = ["g++", "-O2", "-ffp-contract=off", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-o", HOST_TWIN_LIB,
            os.path.join(CSRC, "mpcracing_host.cpp")]
     if verbose:
         print(" ".join(cmd), flush=True)

@@ -1,0 +1,141 @@
+"""Batched centerline geometry on the GPU (the agent's per-tick MPC inputs).
+
+``DeviceTrack`` uploads a track's spline tables once (``mr_track_create``) and
+answers batches of the queries the reference agent runs before every solve
+(agent.py:156-168, 271-274) through the gfx950 kernels of ``csrc/mr_track.h``:
+
+* ``eval``        -- Gx, Gy, dGx, dGy, ddGx, ddGy       splines/ParameterizedLine.py:19-41
+* ``polyfit``     -- x_as_coeffs / y_as_coeffs (deg 4)   ParameterizedLine.py:43-64
+* ``lookup_error``-- lane-table window min             splines/ParameterizedCenterline.py:61-80
+* ``projection``  -- projection_local (bounded Brent)   ParameterizedLine.py:80-97
+* ``frame``       -- unit_tangent yaw, curvature, mean_curvature, unit_principal_normal  :107-149
+* ``error_sign``  -- ParameterizedCenterline.py:82-91
+* ``prep``        -- projection -> coeffs -> max_error, fused (feeds ``BatchSolver`` inputs)
+
+The spline itself is constructed once on the host exactly as the reference does
+(scipy ``make_interp_spline``, ``mpcracing.track.Track``).  There is no CPU
+fallback: without a GPU the constructor raises.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import abi
+from .track import Track, CAR_WIDTH
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class DeviceTrack:
+    def __init__(self, track="shanghai_intl_circuit", device=0):
+        if not torch.cuda.is_available():
+            raise RuntimeError("mpcracing.DeviceTrack needs a ROCm GPU")
+        self.lib = abi.load_product()
+        tr = track if isinstance(track, Track) else Track(track)
+        self.track = tr
+        self.device = torch.device("cuda", int(device))
+        t = np.ascontiguousarray(tr.spline_x.t, dtype=np.float64)
+        cx = np.ascontiguousarray(tr.spline_x.c, dtype=np.float64)
+        cy = np.ascontiguousarray(tr.spline_y.c, dtype=np.float64)
+        if not np.array_equal(tr.spline_y.t, tr.spline_x.t) or tr.spline_x.k != 3:
+            raise ValueError("centerline splines must share cubic knots")
+        ss = np.asarray(tr.err_ss, dtype=np.float64)
+        if not np.array_equal(ss, 0.5 * np.arange(len(ss))):
+            raise ValueError("lane table rows must be s = 0.5 * row (make_lane_width_lookup_table.py)")
+        el = np.ascontiguousarray(tr.err_left, dtype=np.float64)
+        er = np.ascontiguousarray(tr.err_right, dtype=np.float64)
+        P = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))  # noqa: E731
+        h = ctypes.c_void_p()
+        self._check(self.lib.mr_track_create(ctypes.byref(h), int(device), P(t), len(t), P(cx), P(cy), len(cx),
+                                             float(tr.length), P(el), P(er), len(el)))
+        self.h = h
+        self.length = float(tr.length)
+
+    def _check(self, rc):
+        if rc != 0:
+            raise RuntimeError(f"libmpcracing error {rc}: {self.lib.mr_last_error().decode()}")
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            self.lib.mr_track_destroy(h)
+            self.h = None
+
+    def _d(self, a):
+        return torch.as_tensor(np.asarray(a, dtype=np.float64) if not isinstance(a, torch.Tensor) else a,
+                               dtype=torch.float64, device=self.device).reshape(-1).contiguous()
+
+    def _f(self, *shape):
+        return torch.empty(shape, dtype=torch.float64, device=self.device)
+
+    def _i(self, n):
+        return torch.empty(n, dtype=torch.int32, device=self.device)
+
+    def _stream(self, stream):
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        return ctypes.c_void_p(st.cuda_stream)
+
+    def eval(self, s, stream=None):
+        """[6][n] = (Gx, Gy, dGx, dGy, ddGx, ddGy)(s mod L) and the knot span [n]."""
+        s = self._d(s)
+        n = s.numel()
+        out, span = self._f(6, n), self._i(n)
+        self._check(self.lib.mr_track_eval(self.h, n, _ptr(s), _ptr(out), _ptr(span), self._stream(stream)))
+        return out, span
+
+    def frame(self, s, mc_lookahead=45.0, stream=None):
+        s = self._d(s)
+        n = s.numel()
+        yaw, kap, nx, ny, mk = (self._f(n) for _ in range(5))
+        self._check(self.lib.mr_track_frame(self.h, n, _ptr(s), _ptr(yaw), _ptr(kap), _ptr(nx), _ptr(ny),
+                                            float(mc_lookahead), _ptr(mk), self._stream(stream)))
+        return dict(yaw=yaw, curvature=kap, nx=nx, ny=ny, mean_curvature=mk)
+
+    def error_sign(self, X, Y, s, stream=None):
+        X, Y, s = self._d(X), self._d(Y), self._d(s)
+        sg = self._i(s.numel())
+        self._check(self.lib.mr_track_error_sign(self.h, s.numel(), _ptr(X), _ptr(Y), _ptr(s), _ptr(sg),
+                                                 self._stream(stream)))
+        return sg
+
+    def polyfit(self, s, lookahead, stream=None):
+        """x_as_coeffs / y_as_coeffs: cx, cy [5][n], highest order first, global s."""
+        s = self._d(s)
+        la = self._d(np.broadcast_to(np.asarray(lookahead, dtype=np.float64), (s.numel(),)).copy()
+                     if not isinstance(lookahead, torch.Tensor) else lookahead)
+        n = s.numel()
+        cx, cy = self._f(5, n), self._f(5, n)
+        self._check(self.lib.mr_track_polyfit(self.h, n, _ptr(s), _ptr(la), _ptr(cx), _ptr(cy), self._stream(stream)))
+        return cx, cy
+
+    def lookup_error(self, s, lookahead, stream=None):
+        s = self._d(s)
+        n = s.numel()
+        la = self._d(np.broadcast_to(np.asarray(lookahead, dtype=np.float64), (n,)).copy()
+                     if not isinstance(lookahead, torch.Tensor) else lookahead)
+        err, lo, hi, arg = self._f(n), self._i(n), self._i(n), self._i(n)
+        self._check(self.lib.mr_track_lookup_error(self.h, n, _ptr(s), _ptr(la), _ptr(err), _ptr(lo), _ptr(hi),
+                                                   _ptr(arg), self._stream(stream)))
+        return err, lo, hi, arg
+
+    def projection(self, X, Y, lo, hi, stream=None):
+        X, Y, lo, hi = self._d(X), self._d(Y), self._d(lo), self._d(hi)
+        n = X.numel()
+        s, dist, nfev = self._f(n), self._f(n), self._i(n)
+        self._check(self.lib.mr_track_projection(self.h, n, _ptr(X), _ptr(Y), _ptr(lo), _ptr(hi), _ptr(s),
+                                                 _ptr(dist), _ptr(nfev), self._stream(stream)))
+        return s, dist, nfev
+
+    def prep(self, X, Y, lo, hi, lookback=5.0, lookahead=45.0, err_offset=CAR_WIDTH / 2, stream=None):
+        """agent.py tick prep: s, dist, cx, cy [5][n], max_error (lookup_error - car_width/2)."""
+        X, Y, lo, hi = self._d(X), self._d(Y), self._d(lo), self._d(hi)
+        n = X.numel()
+        s, dist, merr = self._f(n), self._f(n), self._f(n)
+        cx, cy = self._f(5, n), self._f(5, n)
+        self._check(self.lib.mr_track_prep(self.h, n, _ptr(X), _ptr(Y), _ptr(lo), _ptr(hi), float(lookback),
+                                           float(lookahead), float(err_offset), _ptr(s), _ptr(dist), _ptr(cx),
+                                           _ptr(cy), _ptr(merr), self._stream(stream)))
+        return dict(s=s, dist=dist, cx=cx, cy=cy, max_error=merr)

@@ -1,0 +1,81 @@
+"""Test helper: the centerline kernels of csrc/mr_track.h built for the host (libmpcracing_host.so).
+TEST-ONLY -- the product path runs them on the GPU (mpcracing.geometry.DeviceTrack)."""
+import ctypes
+import os
+
+import numpy as np
+
+import host_twin as ht
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class HostTrack:
+    """Tables from the reference-generated golden spline (G1) and the repo's lane table."""
+
+    def __init__(self, G, track, rows=None):
+        p = track + "/"
+        self.t = np.ascontiguousarray(G[p + "t"], dtype=np.float64)
+        self.cx = np.ascontiguousarray(G[p + "cx"], dtype=np.float64)
+        self.cy = np.ascontiguousarray(G[p + "cy"], dtype=np.float64)
+        self.L = float(G[p + "L"])
+        d = np.load(os.path.join(REPO, "mpc-racing_amd", "data", "tracks", f"{track}.npz"))
+        assert np.array_equal(d["err_ss"], 0.5 * np.arange(len(d["err_ss"])))
+        self.el = np.ascontiguousarray(d["err_left"][:rows], dtype=np.float64)
+        self.er = np.ascontiguousarray(d["err_right"][:rows], dtype=np.float64)
+        self.lib = ht.lib()
+        self.nt, self.nr = len(self.t), len(self.el)
+        self.blob = np.zeros(self.lib.mrh_track_blob_size(self.nt, self.nr))
+        self.lib.mrh_track_build(_p(self.t), self.nt, _p(self.cx), _p(self.cy), len(self.cx), _p(self.el),
+                                 _p(self.er), self.nr, _p(self.blob))
+
+    def _a(self, x):
+        return np.ascontiguousarray(np.atleast_1d(np.asarray(x, dtype=np.float64)))
+
+    def eval(self, s):
+        s = self._a(s)
+        out, span = np.zeros((6, len(s))), np.zeros(len(s), np.int32)
+        self.lib.mrh_track_eval(_p(self.blob), self.nt, self.L, self.nr, len(s), _p(s), _p(out), _p(span))
+        return out, span
+
+    def frame(self, s, mcla=45.0):
+        s = self._a(s)
+        n = len(s)
+        yaw, kap, nx, ny, mk = (np.zeros(n) for _ in range(5))
+        self.lib.mrh_track_frame(_p(self.blob), self.nt, self.L, self.nr, n, _p(s), _p(yaw), _p(kap), _p(nx),
+                                 _p(ny), float(mcla), _p(mk))
+        return yaw, kap, nx, ny, mk
+
+    def error_sign(self, X, Y, s):
+        X, Y, s = self._a(X), self._a(Y), self._a(s)
+        sg = np.zeros(len(s), np.int32)
+        self.lib.mrh_track_sign(_p(self.blob), self.nt, self.L, self.nr, len(s), _p(X), _p(Y), _p(s), _p(sg))
+        return sg
+
+    def polyfit(self, s, la):
+        s, la = self._a(s), self._a(la)
+        cx, cy = np.zeros((5, len(s))), np.zeros((5, len(s)))
+        self.lib.mrh_track_polyfit(_p(self.blob), self.nt, self.L, self.nr, len(s), _p(s), _p(la), _p(cx), _p(cy))
+        return cx, cy
+
+    def lookup(self, s, la):
+        s, la = self._a(s), self._a(la)
+        n = len(s)
+        err = np.zeros(n)
+        lo, hi, arg = (np.zeros(n, np.int32) for _ in range(3))
+        self.lib.mrh_track_lookup(_p(self.blob), self.nt, self.L, self.nr, n, _p(s), _p(la), _p(err), _p(lo),
+                                  _p(hi), _p(arg))
+        return err, lo, hi, arg
+
+    def projection(self, X, Y, lo, hi):
+        X, Y, lo, hi = self._a(X), self._a(Y), self._a(lo), self._a(hi)
+        n = len(X)
+        s, dist, nf = np.zeros(n), np.zeros(n), np.zeros(n, np.int32)
+        self.lib.mrh_track_projection(_p(self.blob), self.nt, self.L, self.nr, n, _p(X), _p(Y), _p(lo), _p(hi),
+                                      _p(s), _p(dist), _p(nf))
+        return s, dist, nf
