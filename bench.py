@@ -58,6 +58,20 @@ def cpu_baseline(name, budget_s):
                       f"(fp64, tol 1e-8, single thread, {dt:.1f} s)"}
 
 
+def reduce_counters(counts, elapsed, world):
+    """Whole-job totals over the ranks (the only collective of the run): SUM of the per-rank
+    counters [solves, sum of iterations, algorithmic bytes, status histogram...] and MAX of the
+    timed wall clock.  RCCL on the GPU box (backend "nccl"), gloo in the CPU tests."""
+    import torch
+    import torch.distributed as dist
+    tot = counts.to(torch.float64)
+    tmax = torch.tensor([float(elapsed)], dtype=torch.float64, device=tot.device)
+    if world > 1:
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    return tot.cpu().numpy(), float(tmax.item())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -67,6 +81,7 @@ def main():
     ap.add_argument("--per-gpu", type=int, default=None)
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-latency", action="store_true", help="skip the B = 1 latency probe (profiling runs)")
     args = ap.parse_args()
 
     import torch
@@ -124,26 +139,24 @@ def main():
     statuses += stc
 
     # B = 1 latency (same configuration, first instance), p50 of 5 runs
-    b1 = {k: (v[..., :1].copy() if v is not None else None) for k, v in batch.items()}
-    s1 = solver_for_config(args.config, 1, device=local)
-    d1 = s1.to_device(b1)
-    o1 = s1.alloc_outputs(1)
-    lat = []
-    for _ in range(6):
-        torch.cuda.synchronize(dev)
-        t = time.perf_counter()
-        s1.launch(d1, o1, stream)
-        torch.cuda.synchronize(dev)
-        lat.append(time.perf_counter() - t)
-    lat_b1_ms = float(np.median(lat[1:]) * 1e3)
+    lat_b1_ms = None
+    if not args.no_latency:
+        b1 = {k: (v[..., :1].copy() if v is not None else None) for k, v in batch.items()}
+        s1 = solver_for_config(args.config, 1, device=local)
+        d1 = s1.to_device(b1)
+        o1 = s1.alloc_outputs(1)
+        lat = []
+        for _ in range(6):
+            torch.cuda.synchronize(dev)
+            t = time.perf_counter()
+            s1.launch(d1, o1, stream)
+            torch.cuda.synchronize(dev)
+            lat.append(time.perf_counter() - t)
+        lat_b1_ms = float(np.median(lat[1:]) * 1e3)
 
-    tot = torch.tensor([B * args.steps, iters_sum, alg_bytes] + statuses.tolist(), dtype=torch.float64, device=dev)
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    tot = tot.cpu().numpy()
-    elapsed_max = float(tmax.item())
+    tot, elapsed_max = reduce_counters(
+        torch.tensor([B * args.steps, iters_sum, alg_bytes] + statuses.tolist(), dtype=torch.float64, device=dev),
+        elapsed, world)
 
     if rank == 0:
         solves = tot[0]
