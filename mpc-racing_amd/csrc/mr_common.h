@@ -37,6 +37,18 @@ MR_HD float mr_exp(float a) { return expf(a); }
 MR_HD float mr_log(float a) { return logf(a); }
 MR_HD float mr_abs(float a) { return fabsf(a); }
 
+// 1/sqrt(a), a > 0: IEEE in fp64 and on the host; the hardware v_rsq_f32 (1 ulp) on the device
+// in fp32 (the pivots of the Riccati sweep, on its serial critical path)
+MR_HD double mr_rsqrt(double a) { return 1.0 / sqrt(a); }
+#if MR_DEVICE_BUILD
+MR_HD float mr_rsqrt(float a) { return __builtin_amdgcn_rsqf(a); }
+// keep a value computed in every lane (stops the compiler sinking it into per-lane branches)
+#define MR_MATERIALIZE(x) __asm__ volatile("" : "+v"(x))
+#else
+MR_HD float mr_rsqrt(float a) { return 1.0f / sqrtf(a); }
+#define MR_MATERIALIZE(x) ((void)0)
+#endif
+
 template <typename T> MR_HD T mr_max(T a, T b) { return a > b ? a : b; }
 template <typename T> MR_HD T mr_min(T a, T b) { return a < b ? a : b; }
 

@@ -50,10 +50,11 @@ struct RCF {
   enum {
     H = 0, G0 = H + NH, G1 = G0 + NZ, GL = G1 + NZ, J = GL + NZ, C = J + 48, P = C + NX, PV0 = P + NP,
     PV1 = PV0 + NX, K = PV1 + NX, K0 = K + NU * NX, K1 = K0 + NU, ACL = K1 + NU, FF = ACL + NX * NX,
-    JUNK = FF + NX, NF = JUNK + WL
+    CONE = FF + NX, CZERO, SELP, SEL0,  // constants 1, 0, [k > 0], [k == 0] (written once per solve)
+    JUNK, NF                           // discard slot of the branch-free stores (any lane)
   };
 };
-constexpr int RC_STRIDE = 532;
+constexpr int RC_STRIDE = 480;  // words; 16-word (64 B) multiple
 static_assert(RCF::NF <= RC_STRIDE, "record");
 constexpr int64_t WS_WORDS = (int64_t)SSF::NF * WL + (int64_t)RC_STRIDE * WL;
 constexpr int LDS_LD = 17;  // padded row of the 16 x 16 LDS tiles
@@ -106,21 +107,20 @@ MR_HD T row_c(int r, const T* z) { return RN(r) == 1 ? z[RI(r, 0)] : z[RI(r, 0)]
 // 3x3 Cholesky with reciprocal pivots (3 divisions instead of one per substitution step)
 template <typename T>
 MR_HD bool chol3r(const T* R, T* L, T* iv) {
-  if (!(R[0] > T(0))) return false;
-  const T l00 = mr_sqrt(R[0]);
-  iv[0] = T(1) / l00;
+  // branch-free: a non-positive pivot is replaced by 1 and reported (the caller discards L)
+  // (the diagonal of L is only needed through its reciprocals iv)
+  const bool ok0 = R[0] > T(0);
+  iv[0] = mr_rsqrt(ok0 ? R[0] : T(1));
   const T l10 = R[1] * iv[0], l20 = R[2] * iv[0];
   const T d1 = R[3] - l10 * l10;
-  if (!(d1 > T(0))) return false;
-  const T l11 = mr_sqrt(d1);
-  iv[1] = T(1) / l11;
+  const bool ok1 = d1 > T(0);
+  iv[1] = mr_rsqrt(ok1 ? d1 : T(1));
   const T l21 = (R[4] - l20 * l10) * iv[1];
   const T d2 = R[5] - l20 * l20 - l21 * l21;
-  if (!(d2 > T(0))) return false;
-  const T l22 = mr_sqrt(d2);
-  iv[2] = T(1) / l22;
-  L[0] = l00; L[1] = l10; L[2] = l11; L[3] = l20; L[4] = l21; L[5] = l22;
-  return true;
+  const bool ok2 = d2 > T(0);
+  iv[2] = mr_rsqrt(ok2 ? d2 : T(1));
+  L[0] = T(0); L[1] = l10; L[2] = T(0); L[3] = l20; L[4] = l21; L[5] = T(0);
+  return ok0 & ok1 & ok2;
 }
 template <typename T>
 MR_HD void lsolve3r(const T* L, const T* iv, T* b) {
@@ -260,6 +260,11 @@ struct WaveSolver {
         if (act[j]) th += mr_abs(d[j] - s);
       }
       for (int i = 0; i < NX; ++i) { S(SSF::NU + i) = T(0); S(SSF::DNU + i) = T(0); }
+      MR_GLOBAL T* Rk = R(k);  // constant slots of the Riccati gather plan (frag_plan)
+      Rk[RCF::CONE] = T(1);
+      Rk[RCF::CZERO] = T(0);
+      Rk[RCF::SELP] = k > 0 ? T(1) : T(0);
+      Rk[RCF::SEL0] = k > 0 ? T(0) : T(1);
     }
     gmax = wmax(w, gmax);
     th = wsum(w, th);
@@ -467,37 +472,38 @@ struct WaveSolver {
   // frag_load issues the 13 gathers unconditionally one stage ahead, frag_finish applies the
   // selects when the stage is factorised, so no load is sunk into a lane-divergent branch.
   struct FragPlan {
-    int off[13];
-    unsigned data, one_pos, one_k0, dlt;
+    int off[13];  // record offsets: data entries, or the record's constant slots (CONE, CZERO, SELP, SEL0)
+    unsigned dlt;  // D registers on the diagonal of H (+ delta)
     int st_a[4], st_p[4], lp1[4], lp2[4];  // per D register: record / LDS targets (discard slots if none)
   };
   static MR_HD void frag_plan(int lane, FragPlan& fp) {
     const int g = lane >> 4, c = lane & 15;
-    fp.data = fp.one_pos = fp.one_k0 = fp.dlt = 0u;
-    int idx;
-    bool data;
-    T cst;
-    auto put = [&](int q, int i, int j, bool keep) {
+    fp.dlt = 0u;
+    // record slot of entry (i, j) of E^: its data word, or the constant slot holding its value
+    auto src = [&](int i, int j, bool keep) -> int {
+      int idx;
+      bool data;
+      T cst;
+      if (!keep) return RCF::CZERO;
       ehat_src(1, i, j, idx, data, cst);
-      fp.off[q] = idx;
-      if (keep && data) fp.data |= 1u << q;
-      if (keep && cst != T(0)) fp.one_pos |= 1u << q;
+      if (data) return idx;
+      const bool one_pos = cst != T(0);
       ehat_src(0, i, j, idx, data, cst);
-      if (keep && cst != T(0)) fp.one_k0 |= 1u << q;
+      const bool one_k0 = cst != T(0);
+      return one_pos ? (one_k0 ? RCF::CONE : RCF::SELP) : (one_k0 ? RCF::SEL0 : RCF::CZERO);
     };
 #pragma unroll
-    for (int s = 0; s < 4; ++s) put(s, 4 * s + g, c, true);
-    put(4, c, NX + g, (c < NX) & (g < NU));
+    for (int s = 0; s < 4; ++s) fp.off[s] = src(4 * s + g, c, true);
+    fp.off[4] = src(c, NX + g, (c < NX) & (g < NU));
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const int a = drow(g, v);
       const int a_ = a < NZ ? a : 0;
-      fp.off[5 + v] = c < NZ ? RCF::H + hidx(a_, c) : (c == 14 ? RCF::G0 + a_ : RCF::G1 + a_);
-      if (a < NZ) fp.data |= 1u << (5 + v);
-      if (a < NZ && a == c) fp.dlt |= 1u << (5 + v);
-      put(9 + v, a, c, (a < NX) & ((c < NX) | (c == 14)));
+      fp.off[5 + v] = a < NZ ? (c < NZ ? RCF::H + hidx(a_, c) : (c == 14 ? RCF::G0 + a_ : RCF::G1 + a_)) : RCF::CZERO;
+      if (a < NZ && a == c) fp.dlt |= 1u << v;
+      fp.off[9 + v] = src(a, c, (a < NX) & ((c < NX) | (c == 14)));
       // outputs of D register v: closed-loop map, packed-upper P | p0 | p1, LDS image of P^
-      const int junk_r = RCF::JUNK + lane, junk_l = LJUNK_OFF - LP_OFF + lane;  // lp* index from LP
+      const int junk_r = RCF::JUNK, junk_l = LJUNK_OFF - LP_OFF + lane;  // lp* index from LP
       const bool ax = a < NX, up = ax & (c < NX) & (a <= c);
       const bool c14 = ax & (c == 14), c15 = ax & (c == 15);
       fp.st_a[v] = (ax & (c < NX)) ? RCF::ACL + a * NX + c : (c14 ? RCF::FF + a : junk_r);
@@ -510,18 +516,15 @@ struct WaveSolver {
 #pragma unroll
     for (int q = 0; q < 13; ++q) raw[q] = Rk[fp.off[q]];
   }
-  static MR_HD void frag_finish(int k, const FragPlan& fp, T delta, const T* raw, T* eb, T* hc, T& ab, T* ac) {
-    const unsigned one = k > 0 ? fp.one_pos : fp.one_k0;
-    auto val = [&](int q) -> T {
-      return ((fp.data >> q) & 1u) ? raw[q] : (((one >> q) & 1u) ? T(1) : T(0));
-    };
+  // operands straight from the gathered words (constants come from the record's constant slots)
+  static MR_HD void frag_finish(const T* dd, const T* raw, T* eb, T* hc, T& ab, T* ac) {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) eb[s] = val(s);
-    ab = val(4);
+    for (int s = 0; s < 4; ++s) eb[s] = raw[s];
+    ab = raw[4];
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      hc[v] = val(5 + v) + (((fp.dlt >> (5 + v)) & 1u) ? delta : T(0));
-      ac[v] = val(9 + v);
+      hc[v] = raw[5 + v] + dd[v];
+      ac[v] = raw[9 + v];
     }
   }
 
@@ -535,7 +538,7 @@ struct WaveSolver {
   //   A + B K | B (k0 + mu k1) + c        1 x v_mfma
   // Stage k-1's record is gathered (13 loads per lane) while stage k is factorised.
   MR_SWEEP bool riccati(T delta, T mu) {
-    const int l = ln, N = this->N, g = l >> 4, c = l & 15;
+    const int l = ln, N = wu(w, this->N), g = l >> 4, c = l & 15;
     const Wv w = this->w;
     MR_GLOBAL T* const rcb = rc;
     MR_LDS T* const LP = lds + LP_OFF;
@@ -543,29 +546,46 @@ struct WaveSolver {
     auto R = [rcb](int k) { return rcb + (int64_t)k * RC_STRIDE; };
     for (int q = l; q < 16 * LDS_LD; q += WL) LP[q] = T(0);
     wsync_lds(w);
-    if (l < NX) {  // terminal cost-to-go: P_N = H_N,xx + delta I, p_N = g_N
-      MR_GLOBAL T* Rn = R(N);
-      for (int j = 0; j < NX; ++j) {
-        const T v = Rn[RCF::H + hidx(l, j)] + (l == j ? delta : T(0));
-        LP[l * LDS_LD + j] = v;
-        if (j >= l) Rn[RCF::P + pidx(l, j)] = v;
-      }
-      const T p0 = Rn[RCF::G0 + l], p1 = Rn[RCF::G1 + l];
-      LP[l * LDS_LD + 11] = p0;
-      LP[l * LDS_LD + 12] = p1;
-      Rn[RCF::PV0 + l] = p0;
-      Rn[RCF::PV1 + l] = p1;
-    }
-    wsync_lds(w);
     FragPlan fp;
     frag_plan(l, fp);
-    T raw_n[13];
-    frag_load(R(N - 1), fp, raw_n);
-    for (int k = N - 1; k >= 0; --k) {
+    T dd[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) dd[v] = ((fp.dlt >> v) & 1u) ? delta : T(0);
+    // lane-constant 0/1 selectors: per-lane picks as products (exact for finite values), so the
+    // step has no lane-divergent branches
+    const T sg[3] = {g == 0 ? T(1) : T(0), g == 1 ? T(1) : T(0), g == 2 ? T(1) : T(0)};
+    const T sk = ((g < NU) & (c < NX)) ? T(-1) : T(0), sf = ((g < NU) & (c == 14)) ? T(-1) : T(0);
+    T raw_a[13], raw_b[13];
+    frag_load(R(N - 1), fp, raw_a);
+    {  // terminal cost-to-go: P_N = H_N,xx + delta I, p_N = g_N.  Branch-free (lanes >= NX write
+       // discard slots), so at least as many memory ops follow the first prefetch on this path as
+       // on the loop back-edge and the wait at the loop head stays exact.
+      MR_GLOBAL T* Rn = R(N);
+      const bool row = l < NX;
+      const int lr = row ? l : 0, jl = RCF::JUNK, jd = LJUNK_OFF - LP_OFF + l;
+      T hv[NX];  // all loads ahead of the stores (the compiler cannot disambiguate H from P)
+#pragma unroll
+      for (int j = 0; j < NX; ++j) hv[j] = Rn[RCF::H + hidx(lr, j)];
+      const T p0 = Rn[RCF::G0 + lr], p1 = Rn[RCF::G1 + lr];
+#pragma unroll
+      for (int j = 0; j < NX; ++j) {
+        const T v = hv[j] + (l == j ? delta : T(0));
+        LP[row ? l * LDS_LD + j : jd] = v;
+        Rn[(row && j >= l) ? RCF::P + pidx(lr, j) : jl] = v;
+      }
+      LP[row ? l * LDS_LD + 11 : jd] = p0;
+      LP[row ? l * LDS_LD + 12 : jd] = p1;
+      Rn[row ? RCF::PV0 + l : jl] = p0;
+      Rn[row ? RCF::PV1 + l : jl] = p1;
+    }
+    wsync_lds(w);
+    // one stage; the loop below is unrolled by two so the prefetch buffers alternate roles
+    // (no register copies of in-flight loads, hence exact vmcnt waits instead of vmcnt(0))
+    auto step = [&](int k, const T* raw_use, T* raw_fill) -> bool {
       MR_GLOBAL T* Rk = R(k);
       T eb[4], dq[4], dacl[4], ab;
-      frag_finish(k, fp, delta, raw_n, eb, dq, ab, dacl);
-      if (k >= 1) frag_load(R(k - 1), fp, raw_n);
+      frag_finish(dd, raw_use, eb, dq, ab, dacl);
+      frag_load(R(k >= 1 ? k - 1 : 0), fp, raw_fill);  // unconditional: k = 0 re-reads its own record
       // X = P^ E^  (A fragment s: P^[c][4s+g])
       T dx[4] = {T(0), T(0), T(0), T(0)};
 #pragma unroll
@@ -588,7 +608,7 @@ struct WaveSolver {
       auto qat = [&](int a, int b) { return wbcast(w, dq[dreg(a)], dgrp(a) * 16 + b); };
       T Rh[6] = {qat(11, 11), qat(11, 12), qat(11, 13), qat(12, 12), qat(12, 13), qat(13, 13)};
       T L[6], iv[3];
-      if (!chol3r(Rh, L, iv)) return false;  // wave-uniform: same inputs and code on every lane
+      const bool piv_ok = chol3r(Rh, L, iv);  // checked every second stage (below)
       T w0[3] = {qat(11, 14), qat(12, 14), qat(13, 14)};
       T w1[3] = {qat(11, 15), qat(12, 15), qat(13, 15)};
       lsolve3r(L, iv, w0);
@@ -596,7 +616,7 @@ struct WaveSolver {
       T wc[3] = {wshfl(w, dq[dreg(11)], dgrp(11) * 16 + c), wshfl(w, dq[dreg(12)], dgrp(12) * 16 + c),
                  wshfl(w, dq[dreg(13)], dgrp(13) * 16 + c)};
       lsolve3r(L, iv, wc);  // W[:, c]
-      const T wv = g == 0 ? wc[0] : (g == 1 ? wc[1] : (g == 2 ? wc[2] : T(0)));
+      const T wv = wc[0] * sg[0] + wc[1] * sg[1] + wc[2] * sg[2];  // W[g][c] (0 for g = 3)
       T dw[4] = {T(0), T(0), T(0), T(0)};
       wmfma(w, wv, wv, dw);  // W^T W
       // gains: K[:, c] = -L^{-T} W[:, c], feed-forward k0, k1
@@ -604,14 +624,20 @@ struct WaveSolver {
       ltsolve3r(L, iv, kc);
       ltsolve3r(L, iv, k0);
       ltsolve3r(L, iv, k1);
-      if (g == 0 && c < NX)
-        for (int a = 0; a < NU; ++a) Rk[RCF::K + a * NX + c] = -kc[a];
-      if (l == 0)
-        for (int a = 0; a < NU; ++a) { Rk[RCF::K0 + a] = -k0[a]; Rk[RCF::K1 + a] = -k1[a]; }
+      {  // branch-free gain stores (other lanes hit the discard slot): a loop free of divergent
+         // branches keeps the waits for the prefetched operands exact across the back-edge
+        const bool kcol = (g == 0) & (c < NX), l0 = l == 0;
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+          Rk[kcol ? RCF::K + a * NX + c : RCF::JUNK] = -kc[a];
+          Rk[l0 ? RCF::K0 + a : RCF::JUNK] = -k0[a];
+          Rk[l0 ? RCF::K1 + a : RCF::JUNK] = -k1[a];
+        }
+      }
       // closed-loop map (A + B K | B (k0 + mu k1) + c) for the forward recursion
-      const T kg = g == 0 ? kc[0] : (g == 1 ? kc[1] : kc[2]);
-      const T kf = g == 0 ? k0[0] + mu * k1[0] : (g == 1 ? k0[1] + mu * k1[1] : k0[2] + mu * k1[2]);
-      const T kb = g < NU ? (c < NX ? -kg : (c == 14 ? -kf : T(0))) : T(0);
+      const T kg = kc[0] * sg[0] + kc[1] * sg[1] + kc[2] * sg[2];
+      const T kf = (k0[0] + mu * k1[0]) * sg[0] + (k0[1] + mu * k1[1]) * sg[1] + (k0[2] + mu * k1[2]) * sg[2];
+      const T kb = kg * sk + kf * sf;  // -K[g][c] (c < 11), -(k0 + mu k1)[g] (c = 14), else 0
       wmfma(w, ab, kb, dacl);
 #pragma unroll
       for (int v = 0; v < 4; ++v) {  // branch-free: lanes without a target write their discard slot
@@ -622,6 +648,19 @@ struct WaveSolver {
         LP[fp.lp2[v]] = pv;
       }
       wsync_lds(w);
+      return piv_ok;
+    };
+    // Pivots are tested once per stage pair, at the loop latch: a failed stage only costs the
+    // next one, and the loop keeps one back-edge block (exact prefetch waits at the loop head).
+    for (int k = N - 1;; k -= 2) {
+      bool ok = step(k, raw_a, raw_b);
+      if (k == 0) {
+        if (!wuni(w, ok)) return false;
+        break;
+      }
+      ok = step(k - 1, raw_b, raw_a) & ok;
+      if (!wuni(w, ok)) return false;
+      if (k == 1) break;
     }
     wsync(w);  // records (P, K, closed-loop map) visible to every lane
     return true;

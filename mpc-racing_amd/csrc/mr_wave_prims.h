@@ -87,6 +87,21 @@ __device__ __forceinline__ void wmfma(const Wv&, double a, double b, double* d) 
   d[0] = c[0]; d[1] = c[1]; d[2] = c[2]; d[3] = c[3];
 }
 
+// A condition every lane computed identically, made visibly wave-uniform (SGPR) so branches
+// on it stay scalar and the enclosing loop keeps a uniform counter and exact waitcnts.
+__device__ __forceinline__ bool wuni(const Wv&, bool b) { return __builtin_amdgcn_readfirstlane((int)b) != 0; }
+// A value every lane holds identically (e.g. reloaded from the per-lane solver object): SGPR copy
+__device__ __forceinline__ int wu(const Wv&, int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ float wu(const Wv&, float v) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+__device__ __forceinline__ double wu(const Wv&, double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffLL));
+  const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
 // out[i] = value of lane i, i < n (compile-time n): one v_readlane per element
 template <typename T, int n>
 __device__ __forceinline__ void wgather(const Wv& w, T v, T* out) {
@@ -178,6 +193,10 @@ inline void wmfma(const Wv& w, T a, T b, T* d) {
   }
   w.hw->barrier();
 }
+
+inline bool wuni(const Wv&, bool b) { return b; }
+template <typename T>
+inline T wu(const Wv&, T v) { return v; }
 
 template <typename T, int n>
 inline void wgather(const Wv& w, T v, T* out) {
