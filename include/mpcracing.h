@@ -44,6 +44,11 @@ extern "C" {
 #define MR_MODEL_BLENDED_PACEJKA 3 /* blended with learned Pacejka lateral forces            */
 #define MR_MODEL_DYNAMIC_PACEJKA 4 /* dynamic with learned Pacejka lateral forces            */
 
+/* plant models of the closed loop (the numpy simulator-side models) */
+#define MR_PLANT_KINEMATIC 0 /* models/KinematicBicycleModel.py:11-48 */
+#define MR_PLANT_DYNAMIC 1   /* models/DynamicBicycleModel.py:16-78   */
+#define MR_PLANT_BLENDED 2   /* models/BlendedBicycleModel.py:18-58   */
+
 #define MR_PREC_FP64 0
 #define MR_PREC_FP32 1
 
@@ -166,6 +171,25 @@ int mr_track_projection(const mr_track* tr, int32_t n, const double* X, const do
 int mr_track_prep(const mr_track* tr, int32_t n, const double* X, const double* Y, const double* lo,
                   const double* hi, double lookback, double lookahead, double err_offset, double* s,
                   double* dist, double* cx, double* cy, double* max_error, void* hip_stream);
+
+/* ---- closed loop (agent.py:138-314 with a models/ plant in place of CARLA) ---- */
+
+/* One tick of the agent's sensing and MPC-input preparation, per vehicle:
+   progress = projection(X, Y, bounds = progress_bound(prev_progress))   agent.py:80-92, 271-273,
+              ParameterizedLine.py:66-105 (NaN prev_progress or bounds wider than 5 m -> global search;
+              the reference's unseeded dual_annealing is replaced by the best of the bounded Brent over
+              every 5 m window, first minimum wins),
+   error    = dist * error_sign(X, Y, progress)                           agent.py:274,
+   cx, cy   = x/y_as_coeffs(progress - lookback, lookahead)               agent.py:156-165,
+   max_error = lookup_error(progress, lookahead) - err_offset             agent.py:166-168.
+   Arrays [n] (cx, cy [5][n]); prev_progress may be NULL (all global). */
+int mr_agent_sense(const mr_track* tr, int32_t n, const double* X, const double* Y, const double* prev_progress,
+                   double lookback, double lookahead, double err_offset, double* progress, double* error, double* cx,
+                   double* cy, double* max_error, void* hip_stream);
+/* One plant step per vehicle: state [6][n] = (x, y, yaw, v_x, v_y, yaw_dot), cmd [2][n] = (throttle - brake,
+   steer) -> out [6][n] (may alias state).  Model.step(throttle_cmd, steer_cmd, dt) of models/*.py. */
+int mr_plant_step(int32_t model, int32_t n, const double* state, const double* cmd, double dt, double* out,
+                  void* hip_stream);
 
 #ifdef __cplusplus
 }

@@ -10,6 +10,8 @@
 
 #include "mr_wave.h"
 #include "mr_track.h"
+#include "mr_agent.h"
+#include "mr_plant.h"
 #include <vector>
 
 using namespace mr;
@@ -177,6 +179,31 @@ __global__ __launch_bounds__(kTrackBlock) void mr_track_prep_kernel(TrackView T,
   track_polyfit(T, p - lookback, lookahead, a, b);
   for (int j = 0; j < 5; ++j) { cx[(int64_t)j * n + i] = a[j]; cy[(int64_t)j * n + i] = b[j]; }
   merr[i] = lane_lookup(T, p, lookahead, nullptr, nullptr, nullptr) - err_offset;
+}
+
+// Closed-loop pieces (mr_agent.h, mr_plant.h): one lane per vehicle.
+__global__ __launch_bounds__(kTrackBlock) void mr_agent_sense_kernel(TrackView T, int n, const double* X, const double* Y,
+                                                                     const double* prev, double lookback, double lookahead,
+                                                                     double err_offset, double* progress, double* error,
+                                                                     double* cx, double* cy, double* merr) {
+  const int i = blockIdx.x * kTrackBlock + threadIdx.x;
+  if (i >= n) return;
+  AgentSense o;
+  agent_sense(T, X[i], Y[i], prev ? prev[i] : NAN, lookback, lookahead, err_offset, o);
+  progress[i] = o.progress;
+  error[i] = o.error;
+  for (int j = 0; j < 5; ++j) { cx[(int64_t)j * n + i] = o.cx[j]; cy[(int64_t)j * n + i] = o.cy[j]; }
+  merr[i] = o.max_error;
+}
+
+__global__ __launch_bounds__(kTrackBlock) void mr_plant_step_kernel(int model, int n, const double* state,
+                                                                    const double* cmd, double dt, double* out) {
+  const int i = blockIdx.x * kTrackBlock + threadIdx.x;
+  if (i >= n) return;
+  double x[6], o[6];
+  for (int j = 0; j < 6; ++j) x[j] = state[(int64_t)j * n + i];
+  plant_step(model, x, cmd[i], cmd[n + i], dt, o);
+  for (int j = 0; j < 6; ++j) out[(int64_t)j * n + i] = o[j];
 }
 
 extern "C" {
@@ -356,6 +383,26 @@ int mr_track_prep(const mr_track* tr, int32_t n, const double* X, const double* 
                   double* cy, double* max_error, void* hip_stream) {
   if (!X || !Y || !lo || !hi || !s || !dist || !cx || !cy || !max_error) return fail(MR_ERR_ARG, "null argument");
   MR_TRACK_LAUNCH(mr_track_prep_kernel, X, Y, lo, hi, lookback, lookahead, err_offset, s, dist, cx, cy, max_error);
+}
+
+int mr_agent_sense(const mr_track* tr, int32_t n, const double* X, const double* Y, const double* prev_progress,
+                   double lookback, double lookahead, double err_offset, double* progress, double* error, double* cx,
+                   double* cy, double* max_error, void* hip_stream) {
+  if (!X || !Y || !progress || !error || !cx || !cy || !max_error) return fail(MR_ERR_ARG, "null argument");
+  MR_TRACK_LAUNCH(mr_agent_sense_kernel, X, Y, prev_progress, lookback, lookahead, err_offset, progress, error, cx, cy,
+                  max_error);
+}
+
+int mr_plant_step(int32_t model, int32_t n, const double* state, const double* cmd, double dt, double* out,
+                  void* hip_stream) {
+  if (!state || !cmd || !out) return fail(MR_ERR_ARG, "null argument");
+  if (model < MR_PLANT_KINEMATIC || model > MR_PLANT_BLENDED) return fail(MR_ERR_ARG, "unknown plant model");
+  if (n < 0) return fail(MR_ERR_ARG, "n < 0");
+  if (n == 0) return MR_OK;
+  hipLaunchKernelGGL(mr_plant_step_kernel, dim3((n + kTrackBlock - 1) / kTrackBlock), dim3(kTrackBlock), 0,
+                     (hipStream_t)hip_stream, (int)model, (int)n, state, cmd, dt, out);
+  HIP_TRY(hipGetLastError());
+  return MR_OK;
 }
 
 }  // extern "C"

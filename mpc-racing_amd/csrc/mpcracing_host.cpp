@@ -10,6 +10,8 @@
 #include <vector>
 #include "mr_wave.h"
 #include "mr_track.h"
+#include "mr_agent.h"
+#include "mr_plant.h"
 
 using namespace mr;
 
@@ -149,6 +151,30 @@ int mrh_track_projection(const double* blob, int nt, double L, int n_rows, int n
   for (int i = 0; i < n; ++i) {
     s[i] = brent_projection(T, X[i], Y[i], lo[i], hi[i], nfev + i);
     dist[i] = track_dist(T, s[i], X[i], Y[i]);
+  }
+  return 0;
+}
+
+int mrh_agent_sense(const double* blob, int nt, double L, int n_rows, int n, const double* X, const double* Y,
+                    const double* prev, double lookback, double lookahead, double err_offset, double* progress,
+                    double* error, double* cx, double* cy, double* merr) {
+  TrackView T = track_view(blob, nt, L, n_rows);
+  for (int i = 0; i < n; ++i) {
+    AgentSense o;
+    agent_sense(T, X[i], Y[i], prev ? prev[i] : NAN, lookback, lookahead, err_offset, o);
+    progress[i] = o.progress;
+    error[i] = o.error;
+    for (int j = 0; j < 5; ++j) { cx[(int64_t)j * n + i] = o.cx[j]; cy[(int64_t)j * n + i] = o.cy[j]; }
+    merr[i] = o.max_error;
+  }
+  return 0;
+}
+int mrh_plant_step(int model, int n, const double* state, const double* cmd, double dt, double* out) {
+  for (int i = 0; i < n; ++i) {
+    double x[6], o[6];
+    for (int j = 0; j < 6; ++j) x[j] = state[(int64_t)j * n + i];
+    plant_step(model, x, cmd[i], cmd[n + i], dt, o);
+    for (int j = 0; j < 6; ++j) out[(int64_t)j * n + i] = o[j];
   }
   return 0;
 }

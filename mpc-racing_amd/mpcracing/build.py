@@ -9,7 +9,7 @@ import subprocess
 from .abi import CSRC, PRODUCT_LIB, HOST_TWIN_LIB
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-SOURCES = ["mpcracing.hip", "mr_batch.h", "mr_solver.h", "mr_common.h", "gen_dynamics.h", "mr_wave.h", "mr_wave_prims.h", "mr_track.h"]
+SOURCES = ["mpcracing.hip", "mr_batch.h", "mr_solver.h", "mr_common.h", "gen_dynamics.h", "mr_wave.h", "mr_wave_prims.h", "mr_track.h", "mr_agent.h", "mr_plant.h"]
 INCLUDE = os.path.abspath(os.path.join(CSRC, "..", "..", "include"))
 
 

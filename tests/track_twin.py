@@ -79,3 +79,21 @@ class HostTrack:
         self.lib.mrh_track_projection(_p(self.blob), self.nt, self.L, self.nr, n, _p(X), _p(Y), _p(lo), _p(hi),
                                       _p(s), _p(dist), _p(nf))
         return s, dist, nf
+
+    def agent_sense(self, X, Y, prev, lookback=5.0, lookahead=45.0, err_offset=1.85 / 2):
+        X, Y, prev = self._a(X), self._a(Y), self._a(prev)
+        n = len(X)
+        prog, err, merr = np.zeros(n), np.zeros(n), np.zeros(n)
+        cx, cy = np.zeros((5, n)), np.zeros((5, n))
+        self.lib.mrh_agent_sense(_p(self.blob), self.nt, self.L, self.nr, n, _p(X), _p(Y), _p(prev), float(lookback),
+                                 float(lookahead), float(err_offset), _p(prog), _p(err), _p(cx), _p(cy), _p(merr))
+        return prog, err, cx, cy, merr
+
+
+def plant_step(model, state, cmd, dt):
+    """models/*.py Model.step for [6][n] states and [2][n] (throttle - brake, steer) commands."""
+    state = np.ascontiguousarray(state, dtype=np.float64)
+    cmd = np.ascontiguousarray(cmd, dtype=np.float64)
+    out = np.zeros_like(state)
+    ht.lib().mrh_plant_step(int(model), state.shape[1], _p(state), _p(cmd), float(dt), _p(out))
+    return out
