@@ -50,9 +50,11 @@ class ClosedLoop:
         self.lookback, self.lookahead = float(lookback), float(lookahead)
         self.solver = BatchSolver(N, mpc_model, precision, False, Ts, max_batch=self.B, device=device, **solver_kw)
         f = dict(dtype=torch.float64, device=self.dev)
-        # RuntimeControllerParameters (control/ControllerParameters.py:26-32); d_max is the class
-        # attribute the reference reads (MPC.py:50)
-        self.runtime = torch.tensor(runtime, **f).reshape(5, 1).expand(5, self.B).contiguous()
+        # RuntimeControllerParameters (control/ControllerParameters.py:26-32) as (alpha_c, d_max, q_v_y, n,
+        # beta_delta), shared (5 values) or per vehicle ([5][B], e.g. a GA population); the reference's
+        # NLP reads the class attribute d_max (MPC.py:50), which callers reproduce by passing 0.85
+        rt = torch.as_tensor(np.asarray(runtime, dtype=np.float64), **f)
+        self.runtime = (rt.reshape(5, 1).expand(5, self.B) if rt.numel() == 5 else rt.reshape(5, self.B)).contiguous()
         self.sol = self.solver.alloc_outputs(self.B)
         self.progress = torch.empty(self.B, **f)
         self.error = torch.empty(self.B, **f)
