@@ -187,7 +187,7 @@ int mr_agent_sense(const mr_track* tr, int32_t n, const double* X, const double*
                    double lookback, double lookahead, double err_offset, double* progress, double* error, double* cx,
                    double* cy, double* max_error, void* hip_stream);
 /* One plant step per vehicle: state [6][n] = (x, y, yaw, v_x, v_y, yaw_dot), cmd [2][n] = (throttle - brake,
-   steer) -> out [6][n] (may alias state).  Model.step(throttle_cmd, steer_cmd, dt) of models/*.py. */
+   steer) -> out [6][n] (may alias state).  Model.step(throttle_cmd, steer_cmd, dt) of the models/ package. */
 int mr_plant_step(int32_t model, int32_t n, const double* state, const double* cmd, double dt, double* out,
                   void* hip_stream);
 
