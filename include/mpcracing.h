@@ -137,7 +137,8 @@ int64_t mr_workspace_bytes_per_instance(const mr_handle* h);
  * and splines/ParameterizedCenterline.py (lookup_error :61-80, error_sign :82-91).
  * The track is built once on the host, as ParameterizedLine.from_waypoints (:162-178) does: knots
  * t[n_t] and B-spline coefficients cx, cy[n_c] (scipy layout, k = 3), the length L, and the lane
- * table err_left/err_right[n_rows] whose row i is s = 0.5 * i (lanes/<track>_max_error.csv).
+ * table err_left/err_right[n_rows] whose row i is s = 0.5 * i (lanes/<track>_max_error.csv;
+ * n_rows = 0 with NULL tables for a lane boundary, see mr_track_lane_table).
  * All query arrays are caller-owned DEVICE pointers of length n (outputs [m][n] component-major);
  * calls are ordered on hip_stream.  One lane per query. */
 typedef struct mr_track mr_track;
@@ -171,6 +172,17 @@ int mr_track_projection(const mr_track* tr, int32_t n, const double* X, const do
 int mr_track_prep(const mr_track* tr, int32_t n, const double* X, const double* Y, const double* lo,
                   const double* hi, double lookback, double lookahead, double err_offset, double* s,
                   double* dist, double* cx, double* cy, double* max_error, void* hip_stream);
+
+/* ---- lane-width table build -------------------------------------------------
+ * Replaces script/make_lane_width_lookup_table.py:12-16 (Pool(14) over
+ * ParameterizedCenterline.get_errors(lane, s, 0), ParameterizedCenterline.py:41-58, whose
+ * lane.projection with bounds None is projection_global, ParameterizedLine.py:99-105).
+ * `lane` is a lane boundary built like a track (mr_track_create with its own spline from
+ * lanes/<track>_{left,right}.csv, n_rows = 0, err_* NULL).  For each centerline progress s[i]:
+ * dist[i] = min over u in [0, L_lane] of |lane(u) - G(s[i])|, s_lane[i] = that u (may be NULL).
+ * Deterministic global search (mr_track.h lane_distance), one wavefront per query. */
+int mr_track_lane_table(const mr_track* centerline, const mr_track* lane, int32_t n, const double* s, double* dist,
+                        double* s_lane, void* hip_stream);
 
 /* ---- closed loop (agent.py:138-314 with a models/ plant in place of CARLA) ---- */
 

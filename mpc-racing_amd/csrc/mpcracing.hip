@@ -185,6 +185,39 @@ __global__ __launch_bounds__(kTrackBlock) void mr_track_prep_kernel(TrackView T,
 }
 
 // Closed-loop pieces (mr_agent.h, mr_plant.h): one lane per vehicle.
+// Lane-width table build (mr_track.h lane_distance): one wavefront per centerline sample.
+// Lane l scans lane-spline samples m = l, l + 64, ... (knot-interval start / midpoint, span
+// known, no search); the wave arg-min (smallest m on ties, as the serial scan) brackets the
+// bounded-Brent refinement, which lane 0 runs.  The lane tables (~0.5 MB for Shanghai) stay
+// L2-resident across the grid.
+constexpr int kLaneWaves = 4;
+__global__ __launch_bounds__(64 * kLaneWaves) void mr_lane_table_kernel(TrackView C, TrackView lane, int n,
+                                                                       const double* s, double* dist,
+                                                                       double* s_lane) {
+  const int q = blockIdx.x * kLaneWaves + (int)(threadIdx.x >> 6);
+  const int ln = (int)(threadIdx.x & 63);
+  if (q >= n) return;  // wave-uniform
+  double X, Y;
+  centerline_point(C, s[q], &X, &Y);
+  const int M = lane_n_samples(lane);
+  double best = 1e300;
+  int mb = 0x7fffffff;
+  for (int m = ln; m < M; m += 64) {
+    const double d2 = lane_sample_d2(lane, m, X, Y);
+    if (d2 < best) { best = d2; mb = m; }
+  }
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double od = __shfl_xor(best, off);
+    const int om = __shfl_xor(mb, off);
+    if (od < best || (od == best && om < mb)) { best = od; mb = om; }
+  }
+  if (ln == 0) {
+    double u;
+    dist[q] = lane_refine(lane, X, Y, mb, &u);
+    if (s_lane) s_lane[q] = u;
+  }
+}
+
 __global__ __launch_bounds__(kTrackBlock) void mr_agent_sense_kernel(TrackView T, int n, const double* X, const double* Y,
                                                                      const double* prev, double lookback, double lookahead,
                                                                      double err_offset, double* progress, double* error,
@@ -302,8 +335,9 @@ int mr_solve_batch(mr_handle* h, int32_t B, const mr_inputs* in, mr_outputs* out
 
 int mr_track_create(mr_track** out, int32_t device, const double* t, int32_t n_t, const double* cx, const double* cy,
                     int32_t n_c, double length, const double* err_left, const double* err_right, int32_t n_rows) {
-  if (!out || !t || !cx || !cy || !err_left || !err_right) return fail(MR_ERR_ARG, "null argument");
-  if (n_t < 8 || n_c < 4 || n_c > n_t || n_rows < 1 || !(length > 0)) return fail(MR_ERR_ARG, "bad track sizes");
+  if (!out || !t || !cx || !cy) return fail(MR_ERR_ARG, "null argument");
+  if (n_rows > 0 && (!err_left || !err_right)) return fail(MR_ERR_ARG, "null lane table");
+  if (n_t < 8 || n_c < 4 || n_c > n_t || n_rows < 0 || !(length > 0)) return fail(MR_ERR_ARG, "bad track sizes");
   for (int i = 1; i < n_t; ++i)
     if (!(t[i] >= t[i - 1])) return fail(MR_ERR_ARG, "knots not sorted");
   const TrackLayout Lay = track_layout(n_t, n_rows);
@@ -394,6 +428,19 @@ int mr_agent_sense(const mr_track* tr, int32_t n, const double* X, const double*
   if (!X || !Y || !progress || !error || !cx || !cy || !max_error) return fail(MR_ERR_ARG, "null argument");
   MR_TRACK_LAUNCH(mr_agent_sense_kernel, X, Y, prev_progress, lookback, lookahead, err_offset, progress, error, cx, cy,
                   max_error);
+}
+
+int mr_track_lane_table(const mr_track* centerline, const mr_track* lane, int32_t n, const double* s, double* dist,
+                        double* s_lane, void* hip_stream) {
+  if (!centerline || !lane || !s || !dist) return fail(MR_ERR_ARG, "null argument");
+  if (centerline->device != lane->device) return fail(MR_ERR_ARG, "centerline and lane on different devices");
+  if (n < 0) return fail(MR_ERR_ARG, "n < 0");
+  if (n == 0) return MR_OK;
+  HIP_TRY(hipSetDevice(centerline->device));
+  hipLaunchKernelGGL(mr_lane_table_kernel, dim3((n + kLaneWaves - 1) / kLaneWaves), dim3(64 * kLaneWaves), 0,
+                     (hipStream_t)hip_stream, centerline->view, lane->view, (int)n, s, dist, s_lane);
+  HIP_TRY(hipGetLastError());
+  return MR_OK;
 }
 
 int mr_plant_step(int32_t model, int32_t n, const double* state, const double* cmd, double dt, double* out,

@@ -155,6 +155,16 @@ int mrh_track_projection(const double* blob, int nt, double L, int n_rows, int n
   return 0;
 }
 
+// lane-width table build: the serial scan of mr_track.h lane_distance (the kernel's wave scan
+// visits the same samples and breaks ties the same way)
+int mrh_lane_table(const double* cblob, int cnt, double cL, int c_rows, const double* lblob, int lnt, double lL,
+                   int n, const double* s, double* dist, double* s_lane) {
+  TrackView C = track_view(cblob, cnt, cL, c_rows), Ln = track_view(lblob, lnt, lL, 0);
+#pragma omp parallel for schedule(dynamic, 16)
+  for (int i = 0; i < n; ++i) dist[i] = lane_distance(C, Ln, s[i], s_lane ? s_lane + i : nullptr);
+  return 0;
+}
+
 int mrh_agent_sense(const double* blob, int nt, double L, int n_rows, int n, const double* X, const double* Y,
                     const double* prev, double lookback, double lookahead, double err_offset, double* progress,
                     double* error, double* cx, double* cy, double* merr) {

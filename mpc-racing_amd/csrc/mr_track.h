@@ -63,10 +63,16 @@ MR_HD int spline_span(const SplineView& s, double x) {
 }
 
 // de Boor basis (scipy _deBoor_D, m = 0) and the coefficient sum, in scipy's order
+MR_HD double spline_eval_in(const SplineView& s, double x, int ell);
 MR_HD double spline_eval(const SplineView& s, double x, int* span_out = nullptr) {
-  const int k = s.k;
   const int ell = spline_span(s, x);
   if (span_out) *span_out = ell;
+  return spline_eval_in(s, x, ell);
+}
+
+// the same sum with the knot interval ell given (t[ell] <= x < t[ell + 1])
+MR_HD double spline_eval_in(const SplineView& s, double x, int ell) {
+  const int k = s.k;
   double h[4] = {1.0, 0.0, 0.0, 0.0}, hh[4] = {0.0, 0.0, 0.0, 0.0};
   for (int j = 1; j <= k; ++j) {
     for (int q = 0; q < j; ++q) hh[q] = h[q];
@@ -177,6 +183,67 @@ MR_HD double brent_projection(const TrackView& T, double X, double Y, double x1,
   }
   if (nfev) *nfev = num;
   return xf;
+}
+
+// ---- Lane-width table build ----
+// script/make_lane_width_lookup_table.py:12-16 computes, for every centerline sample
+// s = 0.5 i, ParameterizedCenterline.get_errors(lane, s, 0) (ParameterizedCenterline.py:41-58):
+// the distance from G(s) to the lane spline, through lane.projection with bounds None, i.e.
+// projection_global (ParameterizedLine.py:99-105, scipy dual_annealing over [0, L_lane],
+// unseeded).  Deterministic restatement of that global minimum: the lane spline is sampled at
+// the start and the midpoint of every knot interval and at L_lane (sample m: interval
+// k + m / 2, fraction (m & 1) / 2); the nearest sample m* (smallest m on ties) brackets the
+// minimiser in [u_(m*-1), u_(m*+1)] and the bounded Brent (scipy's, as projection_local)
+// refines it there.  The lanes' waypoints are ~0.25 m apart, so the bracket holds the global
+// minimiser; the result matches the reference's committed tables to 1e-4 m (tests).
+MR_HD int lane_n_samples(const TrackView& lane) { return 2 * (lane.x[0].nt - 2 * lane.x[0].k - 1) + 1; }
+
+MR_HD double lane_sample_u(const TrackView& lane, int m, int* ell) {
+  const SplineView& S = lane.x[0];
+  const int nspan = S.nt - 2 * S.k - 1;
+  if (m >= 2 * nspan) { *ell = S.k + nspan - 1; return S.t[S.k + nspan]; }
+  const int l = S.k + (m >> 1);
+  *ell = l;
+  return (m & 1) ? S.t[l] + 0.5 * (S.t[l + 1] - S.t[l]) : S.t[l];
+}
+
+MR_HD double lane_sample_d2(const TrackView& lane, int m, double X, double Y) {
+  int ell;
+  const double u = lane_sample_u(lane, m, &ell);
+  const double dx = spline_eval_in(lane.x[0], u, ell) - X, dy = spline_eval_in(lane.y[0], u, ell) - Y;
+  return dx * dx + dy * dy;
+}
+
+// Brent refinement in the bracket of sample mbest; returns the distance, *s_lane = minimiser
+MR_HD double lane_refine(const TrackView& lane, double X, double Y, int mbest, double* s_lane) {
+  const int M = lane_n_samples(lane);
+  int e;
+  const double lo = lane_sample_u(lane, mbest > 0 ? mbest - 1 : 0, &e);
+  const double hi = lane_sample_u(lane, mbest + 1 < M ? mbest + 1 : M - 1, &e);
+  const double u = brent_projection(lane, X, Y, lo, hi, nullptr);
+  if (s_lane) *s_lane = u;
+  return track_dist(lane, u, X, Y);
+}
+
+// centerline point G(s mod L) (ParameterizedCenterline.get_errors: self.Gx(s), self.Gy(s))
+MR_HD void centerline_point(const TrackView& C, double s, double* X, double* Y) {
+  const double m = py_mod(s, C.L);
+  *X = spline_eval(C.x[0], m);
+  *Y = spline_eval(C.y[0], m);
+}
+
+// serial form (host build, one lane per query): the same samples, scan order and ties
+MR_HD double lane_distance(const TrackView& C, const TrackView& lane, double s, double* s_lane) {
+  double X, Y;
+  centerline_point(C, s, &X, &Y);
+  const int M = lane_n_samples(lane);
+  double best = 1e300;
+  int mb = 0;
+  for (int m = 0; m < M; ++m) {
+    const double d2 = lane_sample_d2(lane, m, X, Y);
+    if (d2 < best) { best = d2; mb = m; }
+  }
+  return lane_refine(lane, X, Y, mb, s_lane);
 }
 
 // lookup_error: min over the 0.5 m rows of [s, s + lookahead) of min(left, right); rows keyed

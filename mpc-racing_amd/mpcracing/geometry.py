@@ -11,6 +11,8 @@ answers batches of the queries the reference agent runs before every solve
 * ``frame``       -- unit_tangent yaw, curvature, mean_curvature, unit_principal_normal  :107-149
 * ``error_sign``  -- ParameterizedCenterline.py:82-91
 * ``prep``        -- projection -> coeffs -> max_error, fused (feeds ``BatchSolver`` inputs)
+* ``lane_errors`` / ``lane_width_table`` -- the offline lane-width table build
+  (script/make_lane_width_lookup_table.py, ParameterizedCenterline.get_errors :41-58)
 
 The spline itself is constructed once on the host exactly as the reference does
 (scipy ``make_interp_spline``, ``mpcracing.track.Track``).  There is no CPU
@@ -59,6 +61,7 @@ class DeviceTrack:
             raise RuntimeError(f"libmpcracing error {rc}: {self.lib.mr_last_error().decode()}")
 
     def __del__(self):
+        self.close_lanes()
         h = getattr(self, "h", None)
         if h is not None and h.value:
             self.lib.mr_track_destroy(h)
@@ -139,3 +142,45 @@ class DeviceTrack:
                                            float(lookahead), float(err_offset), _ptr(s), _ptr(dist), _ptr(cx),
                                            _ptr(cy), _ptr(merr), self._stream(stream)))
         return dict(s=s, dist=dist, cx=cx, cy=cy, max_error=merr)
+
+    # ---- lane-width table build ----
+    def _lane(self, side):
+        lanes = self.__dict__.setdefault("_lanes", {})
+        if side not in lanes:
+            if side not in ("right", "left"):
+                raise ValueError("side is 'right' or 'left'")
+            sx, sy, L = self.track.lane_spline(side)
+            t = np.ascontiguousarray(sx.t, dtype=np.float64)
+            cx = np.ascontiguousarray(sx.c, dtype=np.float64)
+            cy = np.ascontiguousarray(sy.c, dtype=np.float64)
+            P = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))  # noqa: E731
+            h = ctypes.c_void_p()
+            self._check(self.lib.mr_track_create(ctypes.byref(h), self.device.index, P(t), len(t), P(cx), P(cy),
+                                                 len(cx), float(L), None, None, 0))
+            lanes[side] = h
+        return lanes[side]
+
+    def lane_errors(self, side, s, stream=None):
+        """ParameterizedCenterline.get_errors(lane, s_i, 0) for every s_i (ParameterizedCenterline.py:41-58):
+        distance from G(s_i) to the `side` lane boundary (self.right_lane / self.left_lane of the
+        reference, file swap kept), global over the lane.  Returns (dist [n], lane progress [n])."""
+        s = self._d(s)
+        n = s.numel()
+        dist, u = self._f(n), self._f(n)
+        self._check(self.lib.mr_track_lane_table(self.h, self._lane(side), n, _ptr(s), _ptr(dist), _ptr(u),
+                                                 self._stream(stream)))
+        return dist, u
+
+    def lane_width_table(self, step=0.5, stream=None):
+        """script/make_lane_width_lookup_table.py:52-66: ss = arange(0, L, step), right / left errors.
+        Returns numpy (ss, right, left) -- the columns of lanes/<track>_max_error.csv."""
+        ss = np.arange(0, self.length, step=step)
+        right, _ = self.lane_errors("right", ss, stream)
+        left, _ = self.lane_errors("left", ss, stream)
+        return ss, right.cpu().numpy(), left.cpu().numpy()
+
+    def close_lanes(self):
+        for h in self.__dict__.get("_lanes", {}).values():
+            if h.value:
+                self.lib.mr_track_destroy(h)
+        self.__dict__["_lanes"] = {}

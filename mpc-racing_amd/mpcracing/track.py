@@ -29,6 +29,19 @@ def _midpoint(p1, p2, alpha=0.5):
     return (p2[0] - p1[0]) * alpha + p1[0], (p2[1] - p1[1]) * alpha + p1[1]
 
 
+def spline_from_waypoints(xy):
+    """ParameterizedLine.from_waypoints (:162-178): chord-length s accumulated with the reference's
+    Python euclidean, scipy not-a-knot cubic interpolation.  Returns (spline_x, spline_y, length)."""
+    ss = [0.0]
+    cum = 0.0
+    for i in range(len(xy) - 1):
+        cum += _euclidean(xy[i], xy[i + 1])
+        ss.append(cum)
+    s = np.array(ss)
+    xy = np.asarray(xy, dtype=np.float64)
+    return make_interp_spline(s, xy[:, 0]), make_interp_spline(s, xy[:, 1]), ss[-1]
+
+
 class Track:
     def __init__(self, name="shanghai_intl_circuit"):
         d = np.load(os.path.join(TRACK_DIR, f"{name}.npz"))
@@ -56,6 +69,12 @@ class Track:
         # lane boundaries, swapped exactly as ParameterizedCenterline.py:17-21
         self.right_lane_xy = np.stack([d["left_csv_x"], d["left_csv_y"]], 1)
         self.left_lane_xy = np.stack([d["right_csv_x"], d["right_csv_y"]], 1)
+
+    def lane_spline(self, side):
+        """ParameterizedLane.from_file (ParameterizedLane.py:22-25) for self.right_lane / self.left_lane
+        (the file swap kept): (spline_x, spline_y, length) of that lane boundary."""
+        xy = self.right_lane_xy if side == "right" else self.left_lane_xy
+        return spline_from_waypoints([tuple(p) for p in xy.tolist()])
 
     @property
     def knots(self):

@@ -13,8 +13,15 @@ of the reference and the scipy 1.15 algorithms they call:
   third-party dependency, so the oracle calls it on its own spline samples;
 * bounded Brent (scipy ``_minimize_scalar_bounded``, xatol 1e-5, maxiter 500)
   as used by ``projection_local`` (``ParameterizedLine.py:80-97``);
-* ``lookup_error`` with Python round-half-even (``ParameterizedCenterline.py:61-80``).
+* ``lookup_error`` with Python round-half-even (``ParameterizedCenterline.py:61-80``);
+* the lane-width table build (``script/make_lane_width_lookup_table.py:12-16`` ->
+  ``ParameterizedCenterline.get_errors(lane, s, 0)`` :41-58 -> ``projection_global``
+  ``ParameterizedLine.py:99-105``): scipy's ``dual_annealing`` (unseeded) is restated as a
+  deterministic global search -- nearest of the knot-interval start/midpoint samples, then the
+  bounded Brent in its bracket.  Pinned against the reference's committed
+  ``lanes/<track>_max_error.csv`` tables (tests/test_lane_table.py, 1e-4 m).
 """
+import bisect
 import math
 
 import numpy as np
@@ -27,15 +34,17 @@ class Spline:
         self.t = np.asarray(t, dtype=np.float64)
         self.c = np.asarray(c, dtype=np.float64)
         self.k = int(k)
+        self._tl = self.t.tolist()
 
     def span(self, x):
         """Interval index l with t[l] <= x < t[l+1], clamped to [k, n-1] (scipy _find_interval)."""
         t, k = self.t, self.k
         n = len(t) - k - 1
-        l = k
-        while l < n - 1 and x >= t[l + 1]:
-            l += 1
-        return l
+        if x != x:
+            return k
+        # largest l in [k, n-1] with t[l] <= x (bisection on the sorted knots)
+        l = bisect.bisect_right(self._tl, x) - 1
+        return min(max(l, k), n - 1)
 
     def __call__(self, x):
         t, c, k = self.t, self.c, self.k
@@ -232,3 +241,48 @@ def from_golden(g, track):
     """Oracle centerline built from the reference-produced golden spline table (G1)."""
     p = f"{track}/"
     return Centerline(g[p + "t"], g[p + "cx"], g[p + "cy"], float(g[p + "L"]))
+
+
+class Lane:
+    """A lane boundary (ParameterizedLane): the spline of lanes/<track>_{left,right}.csv."""
+
+    def __init__(self, t, cx, cy, length):
+        self.sx = Spline(t, cx, 3)
+        self.sy = Spline(t, cy, 3)
+        self.length = float(length)
+        k = 3
+        nspan = len(self.sx.t) - 2 * k - 1
+        t = self.sx.t
+        u = []
+        for m in range(2 * nspan + 1):  # knot-interval starts and midpoints, then L
+            if m >= 2 * nspan:
+                u.append(float(t[k + nspan]))
+            else:
+                l = k + (m >> 1)
+                u.append(float(t[l] + 0.5 * (t[l + 1] - t[l])) if m & 1 else float(t[l]))
+        self.u = u
+        self.px = np.array([self.sx(q) for q in u])
+        self.py = np.array([self.sy(q) for q in u])
+
+    def dist(self, s, X, Y):
+        m = s % self.length
+        return math.sqrt((self.sx(m) - X) ** 2 + (self.sy(m) - Y) ** 2)
+
+    def distance_global(self, X, Y):
+        """projection_global's minimum distance: nearest sample (first on ties), Brent in its bracket."""
+        dx = self.px - X
+        dy = self.py - Y
+        mb = int(np.argmin(dx * dx + dy * dy))
+        M = len(self.u)
+        lo, hi = self.u[max(mb - 1, 0)], self.u[min(mb + 1, M - 1)]
+        xs = brent_bounded(lambda q: self.dist(q, X, Y), lo, hi)
+        return self.dist(xs, X, Y), xs
+
+
+def lane_errors(center, lane, ss):
+    """ParameterizedCenterline.get_errors(lane, s, 0) for each s (one row of the lane-width table)."""
+    out = []
+    for s in ss:
+        X, Y = center.Gx(float(s)), center.Gy(float(s))
+        out.append(lane.distance_global(X, Y)[0])
+    return np.array(out)

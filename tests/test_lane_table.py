@@ -1,0 +1,104 @@
+"""Lane-width table build: script/make_lane_width_lookup_table.py:12-16 ->
+ParameterizedCenterline.get_errors(lane, s, 0) (:41-58) -> projection_global (ParameterizedLine.py:99-105).
+
+Parity is pinned on the reference's own committed tables lanes/<track>_max_error.csv (carried in
+mpc-racing_amd/data/tracks/<track>.npz as err_right / err_left, produced by the reference with scipy
+dual_annealing): every row of every track within LANE_TOL.  The host build of the kernel source is
+bit-exact with the oracle restatement; the GPU kernel is bit-exact with the host build."""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.dirname(HERE))
+
+import track_twin as tt  # noqa: E402
+from mpcracing.track import Track, TRACKS  # noqa: E402
+from oracle import splines as osp  # noqa: E402
+
+G = np.load(os.path.join(HERE, "golden", "golden.npz"))
+GTRACKS = json.load(open(os.path.join(HERE, "golden", "golden.json")))["tracks"]
+# dual_annealing's own convergence: its local search (L-BFGS-B) stops at ~1e-5 m on t1_triple
+LANE_TOL = 1e-4
+# rows where the reference's unseeded dual_annealing stopped in a local minimum: the global
+# search finds a point of the lane that much closer (t2_triple left row 1493: 8.5807 vs 8.8399 m)
+KNOWN_MISSES = {("t2_triple", "left"): [1493]}
+
+
+def _check_vs_reference(track, side, got, ref):
+    assert (got <= ref + LANE_TOL).all(), (track, side, (got - ref).max())  # never above the reference
+    far = np.where(np.abs(got - ref) >= LANE_TOL)[0].tolist()
+    assert far == KNOWN_MISSES.get((track, side), []), (track, side, far)
+
+
+def _ref_table(track):
+    d = np.load(os.path.join(HERE, "..", "mpc-racing_amd", "data", "tracks", f"{track}.npz"))
+    return d["err_ss"], d["err_right"], d["err_left"]
+
+
+@pytest.mark.parametrize("track", ["shanghai_intl_circuit", "t1_triple"])
+def test_oracle_matches_reference_tables(track):
+    tr = Track(track)
+    center = osp.from_golden(G, track)
+    ss, ref_r, ref_l = _ref_table(track)
+    rows = np.arange(0, len(ss), 37)
+    for side, ref in (("right", ref_r), ("left", ref_l)):
+        sx, sy, L = tr.lane_spline(side)
+        lane = osp.Lane(sx.t, sx.c, sy.c, L)
+        got = osp.lane_errors(center, lane, ss[rows])
+        assert np.abs(got - ref[rows]).max() < LANE_TOL, (side, np.abs(got - ref[rows]).max())
+
+
+@pytest.mark.parametrize("track", TRACKS)
+def test_host_build_matches_reference_tables(track):
+    tr = Track(track)
+    center = tt.HostTrack(G, track) if track in GTRACKS else None
+    if center is None:
+        pytest.skip("no golden centerline for this track")
+    ss, ref_r, ref_l = _ref_table(track)
+    assert np.array_equal(ss, 0.5 * np.arange(len(ss)))  # arange(0, L, 0.5) rows
+    for side, ref in (("right", ref_r), ("left", ref_l)):
+        dist, _ = tt.lane_table(center, tt.HostLane(tr, side), ss)
+        _check_vs_reference(track, side, dist, ref)
+
+
+def test_host_build_bitexact_with_oracle():
+    track = "shanghai_intl_circuit"
+    tr = Track(track)
+    center_o = osp.from_golden(G, track)
+    center_h = tt.HostTrack(G, track)
+    ss = np.r_[0.0, 0.5 * np.arange(1, 3800, 97), 1899.5]
+    for side in ("right", "left"):
+        sx, sy, L = tr.lane_spline(side)
+        lane_o = osp.Lane(sx.t, sx.c, sy.c, L)
+        dist_h, u_h = tt.lane_table(center_h, tt.HostLane(tr, side), ss)
+        for i, s in enumerate(ss):
+            d, u = lane_o.distance_global(center_o.Gx(float(s)), center_o.Gy(float(s)))
+            assert d == dist_h[i] and u == u_h[i], (side, s, d, dist_h[i], u, u_h[i])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("track", ["shanghai_intl_circuit", "t1_triple", "t2_triple"])
+def test_gpu_lane_table(track):
+    torch = pytest.importorskip("torch")
+    from mpcracing.geometry import DeviceTrack
+    d = DeviceTrack(track)
+    ss, ref_r, ref_l = _ref_table(track)
+    torch.cuda.synchronize()
+    import time
+    t0 = time.perf_counter()
+    ss_d, right, left = d.lane_width_table()
+    t1 = time.perf_counter()
+    assert np.array_equal(ss_d, ss)
+    center = tt.HostTrack(G, track)
+    tr = Track(track)
+    for side, got, ref in (("right", right, ref_r), ("left", left, ref_l)):
+        host, _ = tt.lane_table(center, tt.HostLane(tr, side), ss)
+        assert np.array_equal(got, host), (side, np.abs(got - host).max())
+        _check_vs_reference(track, side, got, ref)
+    print(f"{track}: {len(ss)} rows x 2 lanes on the GPU in {1e3 * (t1 - t0):.1f} ms")
+    d.close_lanes()

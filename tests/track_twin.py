@@ -97,3 +97,29 @@ def plant_step(model, state, cmd, dt):
     out = np.zeros_like(state)
     ht.lib().mrh_plant_step(int(model), state.shape[1], _p(state), _p(cmd), float(dt), _p(out))
     return out
+
+
+class HostLane:
+    """A lane boundary spline (mpcracing.track.Track.lane_spline) as host tables (n_rows = 0)."""
+
+    def __init__(self, track, side):
+        sx, sy, L = track.lane_spline(side)
+        self.t = np.ascontiguousarray(sx.t, dtype=np.float64)
+        self.cx = np.ascontiguousarray(sx.c, dtype=np.float64)
+        self.cy = np.ascontiguousarray(sy.c, dtype=np.float64)
+        self.L = float(L)
+        self.lib = ht.lib()
+        self.nt = len(self.t)
+        self.blob = np.zeros(self.lib.mrh_track_blob_size(self.nt, 0))
+        self.lib.mrh_track_build(_p(self.t), self.nt, _p(self.cx), _p(self.cy), len(self.cx), None, None, 0,
+                                 _p(self.blob))
+
+
+def lane_table(center, lane, s):
+    """mr_track.h lane_distance on the host (OpenMP over queries): (dist [n], lane progress [n])."""
+    s = np.ascontiguousarray(np.atleast_1d(np.asarray(s, dtype=np.float64)))
+    n = len(s)
+    dist, u = np.zeros(n), np.zeros(n)
+    center.lib.mrh_lane_table(_p(center.blob), center.nt, center.L, center.nr, _p(lane.blob), lane.nt, lane.L, n,
+                              _p(s), _p(dist), _p(u))
+    return dist, u
