@@ -173,6 +173,15 @@ int mr_track_prep(const mr_track* tr, int32_t n, const double* X, const double* 
                   const double* hi, double lookback, double lookahead, double err_offset, double* s,
                   double* dist, double* cx, double* cy, double* max_error, void* hip_stream);
 
+/* Track construction (host arrays, no device work): ParameterizedLine.from_waypoints
+ * (splines/ParameterizedLine.py:162-178) -- chord-length progress, not-a-knot cubic interpolation
+ * (scipy make_interp_spline, k = 3) -- with ParameterizedCenterline.from_file's closing point
+ * (ParameterizedCenterline.py:93-105) when close_loop.  x, y [n]; outputs t [n + 5] (capacity),
+ * cx, cy [n + 1] (capacity), *n_t = knots written (coefficients: *n_t - 4), *length = L.  The
+ * result feeds mr_track_create. */
+int mr_spline_from_waypoints(const double* x, const double* y, int32_t n, int32_t close_loop, double* t, double* cx,
+                             double* cy, int32_t* n_t, double* length);
+
 /* ---- lane-width table build -------------------------------------------------
  * Replaces script/make_lane_width_lookup_table.py:12-16 (Pool(14) over
  * ParameterizedCenterline.get_errors(lane, s, 0), ParameterizedCenterline.py:41-58, whose

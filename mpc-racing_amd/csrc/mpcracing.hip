@@ -430,6 +430,15 @@ int mr_agent_sense(const mr_track* tr, int32_t n, const double* X, const double*
                   max_error);
 }
 
+int mr_spline_from_waypoints(const double* x, const double* y, int32_t n, int32_t close_loop, double* t, double* cx,
+                             double* cy, int32_t* n_t, double* length) {
+  if (!x || !y || !t || !cx || !cy || !n_t || !length) return fail(MR_ERR_ARG, "null argument");
+  const int np = spline_from_waypoints(x, y, n, close_loop, t, cx, cy, length);
+  if (np < 0) return fail(MR_ERR_ARG, "spline_from_waypoints: need >= 4 distinct waypoints in order");
+  *n_t = np + 4;
+  return MR_OK;
+}
+
 int mr_track_lane_table(const mr_track* centerline, const mr_track* lane, int32_t n, const double* s, double* dist,
                         double* s_lane, void* hip_stream) {
   if (!centerline || !lane || !s || !dist) return fail(MR_ERR_ARG, "null argument");

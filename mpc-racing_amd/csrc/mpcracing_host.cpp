@@ -155,6 +155,14 @@ int mrh_track_projection(const double* blob, int nt, double L, int n_rows, int n
   return 0;
 }
 
+int mrh_spline_from_waypoints(const double* x, const double* y, int n, int close_loop, double* t, double* cx,
+                              double* cy, int* n_t, double* length) {
+  const int np = spline_from_waypoints(x, y, n, close_loop, t, cx, cy, length);
+  if (np < 0) return np;
+  *n_t = np + 4;
+  return 0;
+}
+
 // lane-width table build: the serial scan of mr_track.h lane_distance (the kernel's wave scan
 // visits the same samples and breaks ties the same way)
 int mrh_lane_table(const double* cblob, int cnt, double cL, int c_rows, const double* lblob, int lnt, double lL,

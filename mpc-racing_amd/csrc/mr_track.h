@@ -17,6 +17,7 @@
 // its parity is stated on the fitted values.
 #pragma once
 #include "mr_common.h"
+#include <vector>
 
 namespace mr {
 
@@ -420,6 +421,96 @@ inline void splder_coeffs(const double* t, const double* c, int nt, int k, doubl
   }
   for (int i = m; i < nt - 2; ++i) out[i] = 0.0;
 }
+// ---- Track construction, host side of the library ----
+// ParameterizedLine.from_waypoints (ParameterizedLine.py:162-178): chord-length progress
+// accumulated with the reference's euclidean (splines/util.py:3-4), then scipy
+// make_interp_spline(s, x) (k = 3, not-a-knot: knots [s0]*4 + s[2:-2] + [sL]*4).  The
+// ParameterizedCenterline.from_file closing point (ParameterizedCenterline.py:93-105:
+// midpoint(last, first, alpha = 0.9) when they are more than 0.1 m apart) when close_loop.
+// The collocation system is a B-spline collocation matrix (totally positive), solved by
+// banded Gaussian elimination without pivoting; scipy's gbsv pivots, so coefficients agree
+// to rounding (~1e-12 relative), knots and the arc length bit for bit.
+// Returns the number of points used (n or n + 1); t gets np + 4 knots, cx / cy np coefficients.
+// Python's float ** 2 is libm pow(x, 2.0), which is not always x * x; called through a volatile
+// pointer so the compiler cannot rewrite it into a multiply (splines/util.py:3-4 bit for bit).
+inline double py_square(double x) {
+  static double (*volatile libm_pow)(double, double) = ::pow;
+  return libm_pow(x, 2.0);
+}
+
+inline int spline_from_waypoints(const double* x, const double* y, int n, int close_loop, double* t, double* cx,
+                                 double* cy, double* length) {
+  const int k = 3;
+  if (n < 4) return -1;
+  std::vector<double> px(x, x + n), py(y, y + n);
+  if (close_loop) {
+    const double gx = px[n - 1] - px[0], gy = py[n - 1] - py[0];
+    if (sqrt(py_square(gx) + py_square(gy)) > 0.1) {
+      const double dx = (px[0] - px[n - 1]) * 0.9, dy = (py[0] - py[n - 1]) * 0.9;
+      px.push_back(dx + px[n - 1]);
+      py.push_back(dy + py[n - 1]);
+    }
+  }
+  const int np = (int)px.size();
+  std::vector<double> s(np);
+  double cum = 0.0;
+  s[0] = 0.0;
+  for (int i = 0; i + 1 < np; ++i) {
+    const double ax = px[i] - px[i + 1], ay = py[i] - py[i + 1];
+    cum += sqrt(py_square(ax) + py_square(ay));
+    s[i + 1] = cum;
+  }
+  *length = cum;
+  const int nt = np + 4;
+  for (int i = 0; i <= k; ++i) { t[i] = s[0]; t[nt - 1 - i] = s[np - 1]; }
+  for (int i = 2; i < np - 2; ++i) t[i + 2] = s[i];
+  // collocation rows: B_j(s_i), j = l - 3 .. l; band storage A[i][j - i + KL], KL = KU = 3
+  const int KL = 3, W = 7;
+  std::vector<double> A((size_t)np * W, 0.0), bx(px), by(py);
+  SplineView sv{t, nullptr, nt, k};
+  for (int i = 0; i < np; ++i) {
+    const int l = spline_span(sv, s[i]);
+    double h[4] = {1.0, 0.0, 0.0, 0.0}, hh[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int j = 1; j <= k; ++j) {  // de Boor basis, as spline_eval_in
+      for (int q = 0; q < j; ++q) hh[q] = h[q];
+      h[0] = 0.0;
+      for (int m = 1; m <= j; ++m) {
+        const double xb = t[l + m], xa = t[l + m - j];
+        if (xb == xa) { h[m] = 0.0; continue; }
+        const double w = hh[m - 1] / (xb - xa);
+        h[m - 1] += w * (xb - s[i]);
+        h[m] = w * (s[i] - xa);
+      }
+    }
+    for (int a = 0; a <= k; ++a) {
+      const int col = l - k + a, off = col - i + KL;
+      if (off < 0 || off >= W) return -2;  // outside the band (cannot happen for distinct s)
+      A[(size_t)i * W + off] = h[a];
+    }
+  }
+  for (int j = 0; j < np; ++j) {  // banded LU, no pivoting
+    const double piv = A[(size_t)j * W + KL];
+    if (piv == 0.0) return -3;
+    for (int i = j + 1; i <= j + KL && i < np; ++i) {
+      const double f = A[(size_t)i * W + (j - i + KL)] / piv;
+      if (f == 0.0) continue;
+      for (int c = j; c <= j + KL && c < np; ++c) A[(size_t)i * W + (c - i + KL)] -= f * A[(size_t)j * W + (c - j + KL)];
+      bx[i] -= f * bx[j];
+      by[i] -= f * by[j];
+    }
+  }
+  for (int j = np - 1; j >= 0; --j) {
+    double vx = bx[j], vy = by[j];
+    for (int c = j + 1; c <= j + KL && c < np; ++c) {
+      vx -= A[(size_t)j * W + (c - j + KL)] * cx[c];
+      vy -= A[(size_t)j * W + (c - j + KL)] * cy[c];
+    }
+    cx[j] = vx / A[(size_t)j * W + KL];
+    cy[j] = vy / A[(size_t)j * W + KL];
+  }
+  return np;
+}
+
 inline void track_tables(const double* t, int nt, const double* cx, const double* cy, int nc, const double* el,
                          const double* er, int n_rows, double* blob) {
   const TrackLayout L = track_layout(nt, n_rows);

@@ -31,6 +31,23 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
+def native_spline(lib, x, y, close_loop):
+    """ParameterizedLine.from_waypoints (:162-178) in the library (mr_spline_from_waypoints, host code,
+    no scipy): returns knots t, coefficients cx, cy and the length L."""
+    n = len(x)
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    t, cx, cy = np.zeros(n + 5), np.zeros(n + 1), np.zeros(n + 1)
+    nt, L = ctypes.c_int32(), ctypes.c_double()
+    P = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))  # noqa: E731
+    rc = lib.mr_spline_from_waypoints(P(x), P(y), n, int(close_loop), P(t), P(cx), P(cy), ctypes.byref(nt),
+                                      ctypes.byref(L))
+    if rc != 0:
+        raise RuntimeError(f"mr_spline_from_waypoints: {lib.mr_last_error().decode()}")
+    m = nt.value
+    return t[:m].copy(), cx[:m - 4].copy(), cy[:m - 4].copy(), L.value
+
+
 class DeviceTrack:
     def __init__(self, track="shanghai_intl_circuit", device=0):
         if not torch.cuda.is_available():
@@ -149,10 +166,8 @@ class DeviceTrack:
         if side not in lanes:
             if side not in ("right", "left"):
                 raise ValueError("side is 'right' or 'left'")
-            sx, sy, L = self.track.lane_spline(side)
-            t = np.ascontiguousarray(sx.t, dtype=np.float64)
-            cx = np.ascontiguousarray(sx.c, dtype=np.float64)
-            cy = np.ascontiguousarray(sy.c, dtype=np.float64)
+            xy = self.track.right_lane_xy if side == "right" else self.track.left_lane_xy
+            t, cx, cy, L = native_spline(self.lib, xy[:, 0], xy[:, 1], close_loop=False)
             P = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))  # noqa: E731
             h = ctypes.c_void_p()
             self._check(self.lib.mr_track_create(ctypes.byref(h), self.device.index, P(t), len(t), P(cx), P(cy),

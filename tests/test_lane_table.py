@@ -47,8 +47,8 @@ def test_oracle_matches_reference_tables(track):
     ss, ref_r, ref_l = _ref_table(track)
     rows = np.arange(0, len(ss), 37)
     for side, ref in (("right", ref_r), ("left", ref_l)):
-        sx, sy, L = tr.lane_spline(side)
-        lane = osp.Lane(sx.t, sx.c, sy.c, L)
+        hl = tt.HostLane(tr, side)
+        lane = osp.Lane(hl.t, hl.cx, hl.cy, hl.L)
         got = osp.lane_errors(center, lane, ss[rows])
         assert np.abs(got - ref[rows]).max() < LANE_TOL, (side, np.abs(got - ref[rows]).max())
 
@@ -73,9 +73,9 @@ def test_host_build_bitexact_with_oracle():
     center_h = tt.HostTrack(G, track)
     ss = np.r_[0.0, 0.5 * np.arange(1, 3800, 97), 1899.5]
     for side in ("right", "left"):
-        sx, sy, L = tr.lane_spline(side)
-        lane_o = osp.Lane(sx.t, sx.c, sy.c, L)
-        dist_h, u_h = tt.lane_table(center_h, tt.HostLane(tr, side), ss)
+        hl = tt.HostLane(tr, side)
+        lane_o = osp.Lane(hl.t, hl.cx, hl.cy, hl.L)
+        dist_h, u_h = tt.lane_table(center_h, hl, ss)
         for i, s in enumerate(ss):
             d, u = lane_o.distance_global(center_o.Gx(float(s)), center_o.Gy(float(s)))
             assert d == dist_h[i] and u == u_h[i], (side, s, d, dist_h[i], u, u_h[i])
@@ -102,3 +102,38 @@ def test_gpu_lane_table(track):
         _check_vs_reference(track, side, got, ref)
     print(f"{track}: {len(ss)} rows x 2 lanes on the GPU in {1e3 * (t1 - t0):.1f} ms")
     d.close_lanes()
+
+
+@pytest.mark.parametrize("track", TRACKS)
+def test_native_track_construction(track):
+    """ParameterizedLine.from_waypoints in the library (mr_spline_from_waypoints) vs the reference's
+    own spline (golden G1, built by importing the reference): knots and length bit for bit,
+    coefficients to rounding; the lane boundaries vs scipy make_interp_spline likewise."""
+    d = np.load(os.path.join(HERE, "..", "mpc-racing_amd", "data", "tracks", f"{track}.npz"))
+    wp = d["waypoints"]
+    t, cx, cy, L = tt.native_spline(wp[:, 0], wp[:, 1], close_loop=True)
+    p = track + "/"
+    assert np.array_equal(t, G[p + "t"]) and L == float(G[p + "L"])
+    scale = np.abs(G[p + "cx"]).max() + np.abs(G[p + "cy"]).max()
+    assert np.abs(cx - G[p + "cx"]).max() < 1e-11 * scale and np.abs(cy - G[p + "cy"]).max() < 1e-11 * scale
+    tr = Track(track)
+    for side in ("right", "left"):
+        xy = tr.right_lane_xy if side == "right" else tr.left_lane_xy
+        sx, sy, Ls = tr.lane_spline(side)
+        t, cx, cy, L = tt.native_spline(xy[:, 0], xy[:, 1], close_loop=False)
+        assert np.array_equal(t, sx.t) and L == Ls
+        assert np.abs(cx - sx.c).max() < 1e-9 and np.abs(cy - sy.c).max() < 1e-9, (np.abs(cx - sx.c).max())
+
+
+def test_product_track_construction_matches_host_build():
+    """mr_spline_from_waypoints of libmpcracing.so (host code of the product library; no device
+    work, so it runs without a GPU) equals the host build bit for bit."""
+    from mpcracing import abi
+    from mpcracing.geometry import native_spline
+    lib = abi.load_product()
+    tr = Track("t1_triple")
+    d = np.load(os.path.join(HERE, "..", "mpc-racing_amd", "data", "tracks", "t1_triple.npz"))
+    for xy, close in ((d["waypoints"], True), (tr.left_lane_xy, False)):
+        a = native_spline(lib, xy[:, 0], xy[:, 1], close)
+        b = tt.native_spline(xy[:, 0], xy[:, 1], close)
+        assert all(np.array_equal(u, v) for u, v in zip(a[:3], b[:3])) and a[3] == b[3]

@@ -100,19 +100,33 @@ def plant_step(model, state, cmd, dt):
 
 
 class HostLane:
-    """A lane boundary spline (mpcracing.track.Track.lane_spline) as host tables (n_rows = 0)."""
+    """A lane boundary as host tables (n_rows = 0), built by the library's own
+    mr_spline_from_waypoints (host build), as DeviceTrack does for its lanes."""
 
     def __init__(self, track, side):
-        sx, sy, L = track.lane_spline(side)
-        self.t = np.ascontiguousarray(sx.t, dtype=np.float64)
-        self.cx = np.ascontiguousarray(sx.c, dtype=np.float64)
-        self.cy = np.ascontiguousarray(sy.c, dtype=np.float64)
-        self.L = float(L)
+        xy = track.right_lane_xy if side == "right" else track.left_lane_xy
+        self.t, self.cx, self.cy, self.L = native_spline(xy[:, 0], xy[:, 1], close_loop=False)
         self.lib = ht.lib()
         self.nt = len(self.t)
         self.blob = np.zeros(self.lib.mrh_track_blob_size(self.nt, 0))
         self.lib.mrh_track_build(_p(self.t), self.nt, _p(self.cx), _p(self.cy), len(self.cx), None, None, 0,
                                  _p(self.blob))
+
+
+def native_spline(x, y, close_loop):
+    """mr_track.h spline_from_waypoints (host build): (t, cx, cy, L)."""
+    lib = ht.lib()
+    n = len(x)
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    t, cx, cy = np.zeros(n + 5), np.zeros(n + 1), np.zeros(n + 1)
+    nt, L = ctypes.c_int32(), ctypes.c_double()
+    P = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))  # noqa: E731
+    rc = lib.mrh_spline_from_waypoints(P(x), P(y), n, int(close_loop), P(t), P(cx), P(cy), ctypes.byref(nt),
+                                       ctypes.byref(L))
+    assert rc == 0, rc
+    m = nt.value
+    return t[:m].copy(), cx[:m - 4].copy(), cy[:m - 4].copy(), L.value
 
 
 def lane_table(center, lane, s):
