@@ -45,12 +45,29 @@ static int fail(int code, const std::string& msg) {
 #ifndef MR_WAVES_PER_SIMD
 #define MR_WAVES_PER_SIMD 1
 #endif
+// Option (MR_SS_LDS=1, fp32 only): the per-stage fields (ss, 38.9 KB) live in LDS, so the
+// sweeps' field loads are LDS round trips instead of Infinity-Cache / HBM ones.  Measured on C4:
+// same iterates, B = 1 latency 5.31 -> 4.98 ms, but 44.4 KB of LDS per workgroup leaves 3
+// instances per CU instead of 4 and the 8 192-instance batch takes 107.6 ms instead of 103.5 ms.
+// Off by default.
+#ifndef MR_SS_LDS
+#define MR_SS_LDS 0
+#endif
+template <typename T>
+struct SSInLDS { static constexpr bool value = MR_SS_LDS && sizeof(T) == 4; };
+
 template <typename T, int MODEL>
 __global__ __launch_bounds__(WL, MR_WAVES_PER_SIMD) void mr_wave_kernel(ProbParams<T> P, mr_inputs in, mr_outputs out, int B, T* ws) {
   __shared__ T lds[LDS_WORDS];
   const int i = blockIdx.x;
   Wv w{(int)threadIdx.x};
-  solve_instance_wave<T, MODEL>(P, in, out, B, i, (MR_GLOBAL T*)(ws + (int64_t)i * WS_WORDS), (MR_LDS T*)lds, w);
+  MR_GLOBAL T* wsi = (MR_GLOBAL T*)(ws + (int64_t)i * WS_WORDS);
+  if constexpr (SSInLDS<T>::value) {
+    __shared__ T ssl[SS_WORDS];
+    solve_instance_wave<T, MODEL, true>(P, in, out, B, i, wsi, (MR_LDS T*)lds, w, (MR_LDS T*)ssl);
+  } else {
+    solve_instance_wave<T, MODEL, false>(P, in, out, B, i, wsi, (MR_LDS T*)lds, w, wsi);
+  }
 }
 
 static size_t ws_bytes_per_instance(const mr_config& c) {

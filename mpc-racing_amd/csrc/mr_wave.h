@@ -14,7 +14,8 @@
 //   * the forward substitution (sequential, 11+3 values) runs wave-uniform.
 //
 // Working set per instance (global workspace, base + i * WS_WORDS):
-//   ss[f][64]   per-stage iterate / step fields, lane-contiguous (coalesced per field)
+//   ss[f][64]   per-stage iterate / step fields, lane-contiguous (coalesced per field); the fp32
+//               product kernel keeps them in LDS instead (SSL)
 //   rc[k][336]  per-stage Riccati record (stage Hessian, Jacobian, gradients, P, K)
 #pragma once
 #include "mr_batch.h"
@@ -135,12 +136,22 @@ MR_HD void ltsolve3r(const T* L, const T* iv, T* b) {
   b[0] = (b[0] - L[1] * b[1] - L[3] * b[2]) * iv[0];
 }
 
-template <typename T, int MODEL>
+// Where the per-stage fields ss[f][64] live: global workspace, or (SSL) the workgroup's LDS
+// (fp32: 152 x 64 x 4 B = 38.9 KB, 3 instances per CU).  Same arithmetic either way.
+template <typename T, bool SSL>
+struct SSPtr { typedef MR_GLOBAL T* type; };
+#if MR_DEVICE_BUILD
+template <typename T>
+struct SSPtr<T, true> { typedef MR_LDS T* type; };
+#endif
+constexpr int SS_WORDS = SSF::NF * WL;
+
+template <typename T, int MODEL, bool SSL = false>
 struct WaveSolver {
   const ProbParams<T>& P;
   const Inst<T>& I;
   Wv w;
-  MR_GLOBAL T* ss;
+  typename SSPtr<T, SSL>::type ss;
   MR_GLOBAL T* rc;
   MR_LDS T* lds;
   int N, ln;
@@ -157,10 +168,11 @@ struct WaveSolver {
   int trace_cap = 0;
   unsigned long long tsub[4] = {0, 0, 0, 0};  // diagnostics: sub-phase cycles of the trace instance
 
-  MR_HD WaveSolver(const ProbParams<T>& P_, const Inst<T>& I_, Wv w_, MR_GLOBAL T* ws, MR_LDS T* lds_)
-      : P(P_), I(I_), w(w_), ss(ws), rc(ws + (int64_t)SSF::NF * WL), lds(lds_), N(P_.N), ln(w_.lane) {}
+  MR_HD WaveSolver(const ProbParams<T>& P_, const Inst<T>& I_, Wv w_, MR_GLOBAL T* ws, MR_LDS T* lds_,
+                   typename SSPtr<T, SSL>::type ss_)
+      : P(P_), I(I_), w(w_), ss(ss_), rc(ws + (int64_t)SSF::NF * WL), lds(lds_), N(P_.N), ln(w_.lane) {}
 
-  MR_HD MR_GLOBAL T& S(int f) const { return ss[f * WL + ln]; }
+  MR_HD auto& S(int f) const { return ss[f * WL + ln]; }
   MR_HD MR_GLOBAL T* R(int k) const { return rc + (int64_t)k * RC_STRIDE; }
   MR_HD bool own() const { return ln <= N; }
   MR_HD int zf(int b) const { return b ? SSF::Z1 : SSF::Z0; }
@@ -1012,9 +1024,10 @@ struct WaveSolver {
 };
 
 // Per-instance driver: lane `w.lane` of the wave that solves instance i of the batch.
-template <typename T, int MODEL>
+template <typename T, int MODEL, bool SSL = false>
 MR_HD void solve_instance_wave(const ProbParams<T>& P, const mr_inputs& in, const mr_outputs& out, int64_t B,
-                               int64_t i, MR_GLOBAL T* ws, MR_LDS T* lds, Wv w) {
+                               int64_t i, MR_GLOBAL T* ws, MR_LDS T* lds, Wv w,
+                               typename SSPtr<T, SSL>::type ssp = nullptr) {
   const int N = P.N;
   Inst<T> I;
   const double X0 = in.state0[0 * B + i], Y0 = in.state0[1 * B + i];
@@ -1041,7 +1054,7 @@ MR_HD void solve_instance_wave(const ProbParams<T>& P, const mr_inputs& in, cons
   I.n = (int)in.runtime[3 * B + i];
   if (I.n < 1) I.n = 1;
   I.beta = T(in.runtime[4 * B + i]);
-  WaveSolver<T, MODEL> S(P, I, w, ws, lds);
+  WaveSolver<T, MODEL, SSL> S(P, I, w, ws, lds, SSL ? ssp : (typename SSPtr<T, SSL>::type)ws);
   if (out.trace && out.trace_instance == i) { S.trace = out.trace; S.trace_cap = out.trace_cap; }
   S.init(in.u_init ? in.u_init + i : nullptr, B);
   SolveOut r = S.solve();
