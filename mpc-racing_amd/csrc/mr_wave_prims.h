@@ -109,23 +109,82 @@ __device__ __forceinline__ void wgather(const Wv& w, T v, T* out) {
   for (int i = 0; i < n; ++i) out[i] = wbcast(w, v, i);
 }
 
+// Wave reductions without LDS round trips: butterfly levels 1, 2 as DPP quad permutes, 4 and 8
+// as DPP half-row / row mirrors (the same partners' values once quads / octets agree), 16 and
+// 32 as the gfx950 v_permlane16_swap / v_permlane32_swap.  Every level computes
+// op(own, partner) on every lane, as the xor butterfly does; the host emulation below uses the
+// same partners in the same order, so sums round identically on both.
+__device__ __forceinline__ int dpp_bits(int v, int ctrl_sel) {
+  switch (ctrl_sel) {
+    case 0: return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, true);   // quad_perm [1,0,3,2]
+    case 1: return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, true);   // quad_perm [2,3,0,1]
+    case 2: return __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, true);  // row_half_mirror
+    default: return __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, true); // row_mirror
+  }
+}
+__device__ __forceinline__ int bits_of(int v) { return v; }
+__device__ __forceinline__ int bits_of(float v) { return __float_as_int(v); }
+__device__ __forceinline__ void from_bits(int b, int& v) { v = b; }
+__device__ __forceinline__ void from_bits(int b, float& v) { v = __int_as_float(b); }
+
+template <typename T>
+__device__ __forceinline__ T wdpp(T v, int sel) {
+  if constexpr (sizeof(T) == 8) {
+    const long long b = __double_as_longlong(v);
+    const int lo = dpp_bits((int)(b & 0xffffffffLL), sel), hi = dpp_bits((int)(b >> 32), sel);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+  } else {
+    T r;
+    from_bits(dpp_bits(bits_of(v), sel), r);
+    return r;
+  }
+}
+// (own, partner) of butterfly level 16 (row pairs) or 32 (halves) on every lane
+template <int LEVEL>
+__device__ __forceinline__ void swap_bits(const Wv& w, int v, int& own, int& par) {
+  const auto r = LEVEL == 16 ? __builtin_amdgcn_permlane16_swap(v, v, false, false)
+                             : __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  const bool upper = LEVEL == 16 ? ((w.lane >> 4) & 1) : (w.lane >= 32);
+  own = upper ? (int)r[1] : (int)r[0];
+  par = upper ? (int)r[0] : (int)r[1];
+}
+template <int LEVEL, typename T>
+__device__ __forceinline__ void wswap(const Wv& w, T v, T& own, T& par) {
+  if constexpr (sizeof(T) == 8) {
+    const long long b = __double_as_longlong(v);
+    int ol, pl, oh, ph;
+    swap_bits<LEVEL>(w, (int)(b & 0xffffffffLL), ol, pl);
+    swap_bits<LEVEL>(w, (int)(b >> 32), oh, ph);
+    own = __longlong_as_double(((long long)oh << 32) | (long long)(unsigned)ol);
+    par = __longlong_as_double(((long long)ph << 32) | (long long)(unsigned)pl);
+  } else {
+    int o, q;
+    swap_bits<LEVEL>(w, bits_of(v), o, q);
+    from_bits(o, own);
+    from_bits(q, par);
+  }
+}
+template <typename T, typename Op>
+__device__ __forceinline__ T wreduce(const Wv& w, T v, Op op) {
+#pragma unroll
+  for (int sel = 0; sel < 4; ++sel) v = op(v, wdpp(v, sel));
+  T o, q;
+  wswap<16>(w, v, o, q);
+  v = op(o, q);
+  wswap<32>(w, v, o, q);
+  return op(o, q);
+}
 template <typename T>
 __device__ __forceinline__ T wsum(const Wv& w, T v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v = v + wxor(w, v, m);
-  return v;
+  return wreduce(w, v, [](T a, T b) { return a + b; });
 }
 template <typename T>
 __device__ __forceinline__ T wmax(const Wv& w, T v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) { T o = wxor(w, v, m); v = o > v ? o : v; }
-  return v;
+  return wreduce(w, v, [](T a, T b) { return b > a ? b : a; });
 }
 template <typename T>
 __device__ __forceinline__ T wmin(const Wv& w, T v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) { T o = wxor(w, v, m); v = o < v ? o : v; }
-  return v;
+  return wreduce(w, v, [](T a, T b) { return b < a ? b : a; });
 }
 
 #else  // host fiber emulation -------------------------------------------------------------
@@ -206,7 +265,7 @@ inline void wgather(const Wv& w, T v, T* out) {
   w.hw->barrier();
 }
 
-// butterfly reductions, same association as the device (own + partner at every level)
+// butterfly reductions, same partners and association as the device (own + partner at every level)
 template <typename T, typename Op>
 inline T host_butterfly(const Wv& w, T v, Op op) {
   memcpy(w.hw->buf[w.lane], &v, sizeof(T));
@@ -214,9 +273,15 @@ inline T host_butterfly(const Wv& w, T v, Op op) {
   T vals[WL];
   for (int l = 0; l < WL; ++l) memcpy(&vals[l], w.hw->buf[l], sizeof(T));
   w.hw->barrier();
-  for (int m = 32; m >= 1; m >>= 1) {
+  // the device's partners in the device's order (mr_wave_prims.h wreduce): xor 1, xor 2,
+  // half-row mirror, row mirror, xor 16, xor 32
+  for (int lev = 0; lev < 6; ++lev) {
     T nv[WL];
-    for (int l = 0; l < WL; ++l) nv[l] = op(vals[l], vals[l ^ m]);
+    for (int l = 0; l < WL; ++l) {
+      const int p = lev == 0 ? l ^ 1 : lev == 1 ? l ^ 2 : lev == 2 ? (l & ~7) | (7 - (l & 7))
+                  : lev == 3 ? (l & ~15) | (15 - (l & 15)) : lev == 4 ? l ^ 16 : l ^ 32;
+      nv[l] = op(vals[l], vals[p]);
+    }
     for (int l = 0; l < WL; ++l) vals[l] = nv[l];
   }
   return vals[w.lane];

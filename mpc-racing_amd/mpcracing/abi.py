@@ -78,9 +78,11 @@ def _bind_product(lib):
 _product = None
 
 
-def load_product(path=PRODUCT_LIB):
-    """Load the gfx950 library. There is no fallback: a missing library is an error."""
+def load_product(path=None):
+    """Load the gfx950 library. There is no fallback: a missing library is an error.
+    MR_PRODUCT_LIB may name another build of the same source (developer A/B runs)."""
     global _product
+    path = path or os.environ.get("MR_PRODUCT_LIB") or PRODUCT_LIB
     if _product is None:
         if not os.path.exists(path):
             raise RuntimeError(f"libmpcracing.so not built ({path}); run `python __graft_entry__.py build`")
