@@ -698,7 +698,10 @@ struct WaveSolver {
       T dxi = T(0);
       if (ln < NX) LDX[ln] = T(0);
       // row i of the closed-loop map and f[i], prefetched PD stages ahead (register ring)
-      constexpr int PD = 4;
+#ifndef MR_FWD_PD
+#define MR_FWD_PD 4
+#endif
+      constexpr int PD = MR_FWD_PD;
       T ar_r[PD][NX], f_r[PD];
 #pragma unroll
       for (int d = 0; d < PD; ++d) {

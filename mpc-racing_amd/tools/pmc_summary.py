@@ -1,6 +1,9 @@
 """Summarise rocprofv3 outputs of a bench run into profiles/ (developer tool).
 
-usage: pmc_summary.py <stats_csv> <fetch_counter_csv> <write_counter_csv> <out_json> [kernel_substr]
+usage: pmc_summary.py <stats_csv> <fetch_counter_csv> <write_counter_csv> <out_json> [kernel_substr] [B] [config]
+
+B / config are recorded so bench.py can match the summary to its own batch (it reports
+`traffic` only when B agrees).
 
 HBM traffic per launch of the dominant kernel, corrected as MI355X_MICROARCH.md §HBM prescribes:
 FETCH_SIZE (KiB) reports half of the bytes of wide coalesced reads on gfx950 -> x2; WRITE_SIZE
@@ -49,6 +52,12 @@ def main():
     if f is not None and w is not None:
         res["hbm_bytes_per_launch"] = (2.0 * f + w) * 1024.0
     res["dispatches"] = [nf, nw]
+    if len(sys.argv) > 6:
+        res["B"] = int(sys.argv[6])
+    if len(sys.argv) > 7:
+        res["config"] = sys.argv[7]
+        res["command"] = ("rocprofv3 --pmc FETCH_SIZE|WRITE_SIZE (separate passes) -- python bench.py --config "
+                          f"{sys.argv[7]} --steps 1 --warmup 0 --no-cpu-baseline --no-latency")
     with open(out, "w") as fo:
         json.dump(res, fo, indent=1)
     print(json.dumps(res))
