@@ -62,11 +62,21 @@ __global__ __launch_bounds__(WL, MR_WAVES_PER_SIMD) void mr_wave_kernel(ProbPara
   const int i = blockIdx.x;
   Wv w{(int)threadIdx.x};
   MR_GLOBAL T* wsi = (MR_GLOBAL T*)(ws + (int64_t)i * WS_WORDS);
-  if constexpr (SSInLDS<T>::value) {
+  // wave-uniform problem and instance constants in LDS: the non-inlined sweeps reach them through
+  // generic references, which would otherwise resolve to the private stack (scratch) copy
+  __shared__ ProbParams<T> Psh;
+  __shared__ Inst<T> Ish;
+  if (threadIdx.x == 0) Psh = P;
+  __syncthreads();
+  // one solver object per lane (its wave-uniform iteration state), also in LDS
+  constexpr bool SSL = SSInLDS<T>::value;
+  __shared__ alignas(16) char slots[WL * sizeof(WaveSolver<T, MODEL, SSL>)];
+  if constexpr (SSL) {
     __shared__ T ssl[SS_WORDS];
-    solve_instance_wave<T, MODEL, true>(P, in, out, B, i, wsi, (MR_LDS T*)lds, w, (MR_LDS T*)ssl);
+    solve_instance_wave<T, MODEL, true, true>(Psh, in, out, B, i, wsi, (MR_LDS T*)lds, w, (MR_LDS T*)ssl, &Ish,
+                                              slots);
   } else {
-    solve_instance_wave<T, MODEL, false>(P, in, out, B, i, wsi, (MR_LDS T*)lds, w, wsi);
+    solve_instance_wave<T, MODEL, false, true>(Psh, in, out, B, i, wsi, (MR_LDS T*)lds, w, wsi, &Ish, slots);
   }
 }
 

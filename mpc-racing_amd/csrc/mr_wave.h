@@ -18,6 +18,8 @@
 //               product kernel keeps them in LDS instead (SSL)
 //   rc[k][336]  per-stage Riccati record (stage Hessian, Jacobian, gradients, P, K)
 #pragma once
+#include <new>
+
 #include "mr_batch.h"
 #include "mr_wave_prims.h"
 
@@ -37,6 +39,21 @@
 #define MR_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)
 #else
 #define MR_SCHED_BARRIER() ((void)0)
+#endif
+
+// Device sweeps are non-inlined member functions: `this` (the solver object) and the problem /
+// instance constants it references live in LDS (mpcracing.hip), which the compiler cannot see
+// through the generic pointers; the assumption lets it emit ds_read instead of flat loads.
+// (mr_wave_kernel is the only device user of WaveSolver and always places it so.)
+#if MR_DEVICE_BUILD && defined(__HIP_DEVICE_COMPILE__)
+#define MR_ASSUME_LDS_STATE()                                      \
+  do {                                                             \
+    __builtin_assume(__builtin_amdgcn_is_shared((const void*)this));  \
+    __builtin_assume(__builtin_amdgcn_is_shared((const void*)&P));    \
+    __builtin_assume(__builtin_amdgcn_is_shared((const void*)&I));    \
+  } while (0)
+#else
+#define MR_ASSUME_LDS_STATE() ((void)0)
 #endif
 
 namespace mr {
@@ -291,6 +308,7 @@ struct WaveSolver {
 
   // ---------------- sweep 1: evaluation, KKT error terms, stage QP data (lane = stage) ----------------
   MR_SWEEP void eval_sweep(T mu_prev) {
+    MR_ASSUME_LDS_STATE();
     const T kappa_sigma = T(1e10);
     const int k = ln;
     T st_l = T(0), pr_l = T(0), th_l = T(0), smax_l = T(0), smin_l = T(1e30), nu1_l = T(0), lam1_l = T(0),
@@ -550,6 +568,7 @@ struct WaveSolver {
   //   A + B K | B (k0 + mu k1) + c        1 x v_mfma
   // Stage k-1's record is gathered (13 loads per lane) while stage k is factorised.
   MR_SWEEP bool riccati(T delta, T mu) {
+    MR_ASSUME_LDS_STATE();
     const int l = ln, N = wu(w, this->N), g = l >> 4, c = l & 15;
     const Wv w = this->w;
     MR_GLOBAL T* const rcb = rc;
@@ -683,6 +702,7 @@ struct WaveSolver {
   //   i < 11 owns dx[i], the 11 values are shared with v_readlane, one 11-term dot per step.
   //   Then stage-parallel: du_k = K_k dx_k + k0 + mu k1, slack/dual steps, costates.
   MR_SWEEP void forward(T& ap, T& ad, T& gphi) {
+    MR_ASSUME_LDS_STATE();
     const unsigned long long tf0 = trace ? MR_CLOCK() : 0ull;
     const T mu = this->mu;
     const T tau = mr_max(T(0.99), T(1) - mu);
@@ -802,6 +822,7 @@ struct WaveSolver {
 
   // ---------------- sweep 4: line-search trial point (writes buffer 1-cur) ----------------
   MR_SWEEP bool trial(T alpha, bool soc, T& th_t, T& ph_t) {
+    MR_ASSUME_LDS_STATE();
     const int nb = 1 - cur;
     const int k = ln;
     T z[NZS], zt[NZS], zpl[NZS];
@@ -1027,12 +1048,21 @@ struct WaveSolver {
 };
 
 // Per-instance driver: lane `w.lane` of the wave that solves instance i of the batch.
-template <typename T, int MODEL, bool SSL = false>
+// Ish: where the instance constants live -- the workgroup's LDS on the device (every lane writes
+// the same values), so the sweeps read them with LDS latency instead of private-stack latency;
+// nullptr = a local (host build).
+template <typename Solver>
+MR_HD void run_instance(Solver& S, const mr_inputs& in, const mr_outputs& out, int64_t B, int64_t i, int N,
+                        double X0, double Y0, double s0, Wv w);
+
+template <typename T, int MODEL, bool SSL = false, bool OBJ_LDS = false>
 MR_HD void solve_instance_wave(const ProbParams<T>& P, const mr_inputs& in, const mr_outputs& out, int64_t B,
                                int64_t i, MR_GLOBAL T* ws, MR_LDS T* lds, Wv w,
-                               typename SSPtr<T, SSL>::type ssp = nullptr) {
+                               typename SSPtr<T, SSL>::type ssp = nullptr, Inst<T>* Ish = nullptr,
+                               void* solver_slots = nullptr) {
   const int N = P.N;
-  Inst<T> I;
+  Inst<T> Iloc;
+  Inst<T>& I = Ish ? *Ish : Iloc;
   const double X0 = in.state0[0 * B + i], Y0 = in.state0[1 * B + i];
   const double s0 = in.s0[i];
   I.x0[0] = T(0);
@@ -1057,7 +1087,30 @@ MR_HD void solve_instance_wave(const ProbParams<T>& P, const mr_inputs& in, cons
   I.n = (int)in.runtime[3 * B + i];
   if (I.n < 1) I.n = 1;
   I.beta = T(in.runtime[4 * B + i]);
-  WaveSolver<T, MODEL, SSL> S(P, I, w, ws, lds, SSL ? ssp : (typename SSPtr<T, SSL>::type)ws);
+#if MR_DEVICE_BUILD
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the LDS copy is written before any lane reads it
+  __builtin_amdgcn_wave_barrier();
+#endif
+  typedef WaveSolver<T, MODEL, SSL> Solver;
+  const typename SSPtr<T, SSL>::type ssv = SSL ? ssp : (typename SSPtr<T, SSL>::type)ws;
+  if constexpr (OBJ_LDS) {
+    // the solver object (a per-lane copy of the wave-uniform iteration state) in the caller's LDS
+    // slots: the non-inlined sweeps reach it through `this`, which would otherwise point into the
+    // private stack, whose loads take Infinity-Cache / HBM latency
+    Solver* Sp = new ((char*)solver_slots + (size_t)w.lane * sizeof(Solver)) Solver(P, I, w, ws, lds, ssv);
+    run_instance(*Sp, in, out, B, i, N, X0, Y0, s0, w);
+  } else {
+    Solver S(P, I, w, ws, lds, ssv);
+    run_instance(S, in, out, B, i, N, X0, Y0, s0, w);
+  }
+}
+
+template <typename Solver>
+MR_HD void run_instance(Solver& S, const mr_inputs& in, const mr_outputs& out, int64_t B, int64_t i, int N,
+                        double X0, double Y0, double s0, Wv w) {
+  typedef decltype(S.mu) T;
+  const ProbParams<T>& P = S.P;
+  const Inst<T>& I = S.I;
   if (out.trace && out.trace_instance == i) { S.trace = out.trace; S.trace_cap = out.trace_cap; }
   S.init(in.u_init ? in.u_init + i : nullptr, B);
   SolveOut r = S.solve();
