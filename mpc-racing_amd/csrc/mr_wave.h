@@ -181,6 +181,9 @@ struct WaveSolver {
   int nfilt;
   T stat_max, pr_max, theta, slam_max, slam_min, nu1, lam1, fval, logs;
   int me, mi;
+  // out-parameters of the non-inlined sweeps: members, so they land in the object's LDS slot
+  // rather than in the caller's private stack (a scratch round trip after every call)
+  T res_ap, res_ad, res_gphi, res_th, res_ph;
   double* trace = nullptr;
   int trace_cap = 0;
   unsigned long long tsub[4] = {0, 0, 0, 0};  // diagnostics: sub-phase cycles of the trace instance
@@ -966,7 +969,7 @@ struct WaveSolver {
       MR_T1(1);
       if (!fact_ok) { out.status = 3; break; }
       if (delta > T(0)) delta_last = delta;
-      T ap, ad, gphi;
+      T &ap = res_ap, &ad = res_ad, &gphi = res_gphi;
       MR_T0();
       forward(ap, ad, gphi);
       MR_T1(2);
@@ -986,7 +989,7 @@ struct WaveSolver {
       while (alpha >= a_min) {
         for (int pass = 0; pass < 2 && !accepted; ++pass) {
           bool soc = pass == 1;
-          T th_t, ph_t;
+          T &th_t = res_th, &ph_t = res_ph;
           MR_T0();
           bool ok = trial(alpha, soc, th_t, ph_t);
           MR_T1(3);
@@ -1012,7 +1015,7 @@ struct WaveSolver {
       }
       if (!accepted) {
         alpha = mr_max(alpha, a_min);
-        T th_t, ph_t;
+        T &th_t = res_th, &ph_t = res_ph;
         trial(alpha, false, th_t, ph_t);
         ftype = false;
       }
