@@ -71,12 +71,14 @@ __global__ __launch_bounds__(WL, MR_WAVES_PER_SIMD) void mr_wave_kernel(ProbPara
   // one solver object per lane (its wave-uniform iteration state), also in LDS
   constexpr bool SSL = SSInLDS<T>::value;
   __shared__ alignas(16) char slots[WL * sizeof(WaveSolver<T, MODEL, SSL>)];
+  __shared__ T filt_sh[2 * FMAX];  // the line-search filter, shared by the wave
   if constexpr (SSL) {
     __shared__ T ssl[SS_WORDS];
     solve_instance_wave<T, MODEL, true, true>(Psh, in, out, B, i, wsi, (MR_LDS T*)lds, w, (MR_LDS T*)ssl, &Ish,
-                                              slots);
+                                              slots, (MR_LDS T*)filt_sh);
   } else {
-    solve_instance_wave<T, MODEL, false, true>(Psh, in, out, B, i, wsi, (MR_LDS T*)lds, w, wsi, &Ish, slots);
+    solve_instance_wave<T, MODEL, false, true>(Psh, in, out, B, i, wsi, (MR_LDS T*)lds, w, wsi, &Ish, slots,
+                                               (MR_LDS T*)filt_sh);
   }
 }
 

@@ -177,7 +177,14 @@ struct WaveSolver {
   T mu, sc, delta_last;
   T alpha_p, alpha_d;
   T theta_max, theta_min;
-  T filt_th[FMAX], filt_ph[FMAX];
+#if MR_DEVICE_BUILD
+  // the filter is wave-uniform: one copy per workgroup in LDS (set by mr_wave_kernel), every
+  // lane writing the same values, instead of one copy per lane in the solver object
+  MR_LDS T* filt;
+#else
+  T filt_store[2 * FMAX];
+  T* filt = filt_store;
+#endif
   int nfilt;
   T stat_max, pr_max, theta, slam_max, slam_min, nu1, lam1, fval, logs;
   int me, mi;
@@ -193,6 +200,8 @@ struct WaveSolver {
       : P(P_), I(I_), w(w_), ss(ss_), rc(ws + (int64_t)SSF::NF * WL), lds(lds_), N(P_.N), ln(w_.lane) {}
 
   MR_HD auto& S(int f) const { return ss[f * WL + ln]; }
+  MR_HD auto& fth(int i) const { return filt[i]; }
+  MR_HD auto& fph(int i) const { return filt[FMAX + i]; }
   MR_HD MR_GLOBAL T* R(int k) const { return rc + (int64_t)k * RC_STRIDE; }
   MR_HD bool own() const { return ln <= N; }
   MR_HD int zf(int b) const { return b ? SSF::Z1 : SSF::Z0; }
@@ -898,18 +907,18 @@ struct WaveSolver {
 
   MR_HD bool filter_ok(T th, T ph) const {
     for (int i = 0; i < FMAX; ++i)
-      if (i < nfilt && th >= filt_th[i] && ph >= filt_ph[i]) return false;
+      if (i < nfilt && th >= fth(i) && ph >= fph(i)) return false;
     return true;
   }
   MR_HD void filter_add(T th, T ph) {
     if (nfilt < FMAX) {
       for (int i = 0; i < FMAX; ++i)
-        if (i == nfilt) { filt_th[i] = th; filt_ph[i] = ph; }
+        if (i == nfilt) { fth(i) = th; fph(i) = ph; }
       nfilt++;
     } else {
-      for (int i = 0; i < FMAX - 1; ++i) { filt_th[i] = filt_th[i + 1]; filt_ph[i] = filt_ph[i + 1]; }
-      filt_th[FMAX - 1] = th;
-      filt_ph[FMAX - 1] = ph;
+      for (int i = 0; i < FMAX - 1; ++i) { fth(i) = fth(i + 1); fph(i) = fph(i + 1); }
+      fth(FMAX - 1) = th;
+      fph(FMAX - 1) = ph;
     }
   }
 
@@ -1062,7 +1071,7 @@ template <typename T, int MODEL, bool SSL = false, bool OBJ_LDS = false>
 MR_HD void solve_instance_wave(const ProbParams<T>& P, const mr_inputs& in, const mr_outputs& out, int64_t B,
                                int64_t i, MR_GLOBAL T* ws, MR_LDS T* lds, Wv w,
                                typename SSPtr<T, SSL>::type ssp = nullptr, Inst<T>* Ish = nullptr,
-                               void* solver_slots = nullptr) {
+                               void* solver_slots = nullptr, MR_LDS T* filt_sh = nullptr) {
   const int N = P.N;
   Inst<T> Iloc;
   Inst<T>& I = Ish ? *Ish : Iloc;
@@ -1101,6 +1110,9 @@ MR_HD void solve_instance_wave(const ProbParams<T>& P, const mr_inputs& in, cons
     // slots: the non-inlined sweeps reach it through `this`, which would otherwise point into the
     // private stack, whose loads take Infinity-Cache / HBM latency
     Solver* Sp = new ((char*)solver_slots + (size_t)w.lane * sizeof(Solver)) Solver(P, I, w, ws, lds, ssv);
+#if MR_DEVICE_BUILD
+    Sp->filt = filt_sh;
+#endif
     run_instance(*Sp, in, out, B, i, N, X0, Y0, s0, w);
   } else {
     Solver S(P, I, w, ws, lds, ssv);
