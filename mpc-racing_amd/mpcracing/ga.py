@@ -83,31 +83,5 @@ def rewards(times, avg_times):
     return r, avg
 
 
-class TrackSegments:
-    """splines/TrackSegments.py:7-35 on the host Track (scipy quad / fsolve, as the reference):
-    ``n_cp`` segments of equal model lap time, curve speed min(v_max, sqrt(radius * curve_c)) with
-    the reference's radius formula 1 / |(G'x - G'y) G''y| kept as written."""
-
-    def __init__(self, track, n_cp, v_max, d_f, d_r, m):
-        from scipy import integrate, optimize
-        self._quad, self._fsolve = integrate.quad, optimize.fsolve
-        self.line, self.n_cp, self.v_max = track, n_cp, v_max
-        self.curve_c = (2 * d_f + 2 * d_r) / m
-        self.lap_time = self.segment_time(0, track.length)
-        self.bounds = self.calculate_segment_bounds()
-
-    def curve_radius(self, s):
-        return 1 / abs((self.line.dGx(s) - self.line.dGy(s)) * self.line.ddGy(s))
-
-    def curve_velocity(self, s):
-        return min(self.v_max, np.sqrt(self.curve_radius(s) * self.curve_c))
-
-    def segment_time(self, s_0, s_1):
-        return self._quad(lambda x: 1 / self.curve_velocity(x), s_0, s_1, limit=500)[0]
-
-    def calculate_segment_bounds(self):
-        bounds = [0]
-        for _ in range(self.n_cp):
-            b = self._fsolve(lambda x: self.segment_time(bounds[-1], x) - (self.lap_time / self.n_cp), bounds[-1])[0]
-            bounds.append(float(b))
-        return bounds
+# splines/TrackSegments.py:7-35, the drop-in module (host quadrature, reference formulas)
+from splines.TrackSegments import TrackSegments  # noqa: E402,F401

@@ -49,29 +49,38 @@ def native_spline(lib, x, y, close_loop):
 
 
 class DeviceTrack:
-    def __init__(self, track="shanghai_intl_circuit", device=0):
+    def __init__(self, track="shanghai_intl_circuit", device=0, tables=None):
+        """``track``: a track name or ``mpcracing.track.Track``; or ``tables`` = (t, cx, cy, L,
+        err_left, err_right) for a spline built elsewhere (the drop-in ParameterizedLine's
+        ``from_waypoints``; lane tables may be None)."""
         if not torch.cuda.is_available():
             raise RuntimeError("mpcracing.DeviceTrack needs a ROCm GPU")
         self.lib = abi.load_product()
-        tr = track if isinstance(track, Track) else Track(track)
-        self.track = tr
         self.device = torch.device("cuda", int(device))
-        t = np.ascontiguousarray(tr.spline_x.t, dtype=np.float64)
-        cx = np.ascontiguousarray(tr.spline_x.c, dtype=np.float64)
-        cy = np.ascontiguousarray(tr.spline_y.c, dtype=np.float64)
-        if not np.array_equal(tr.spline_y.t, tr.spline_x.t) or tr.spline_x.k != 3:
-            raise ValueError("centerline splines must share cubic knots")
-        ss = np.asarray(tr.err_ss, dtype=np.float64)
-        if not np.array_equal(ss, 0.5 * np.arange(len(ss))):
-            raise ValueError("lane table rows must be s = 0.5 * row (make_lane_width_lookup_table.py)")
-        el = np.ascontiguousarray(tr.err_left, dtype=np.float64)
-        er = np.ascontiguousarray(tr.err_right, dtype=np.float64)
-        P = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))  # noqa: E731
+        if tables is None:
+            tr = track if isinstance(track, Track) else Track(track)
+            self.track = tr
+            if not np.array_equal(tr.spline_y.t, tr.spline_x.t) or tr.spline_x.k != 3:
+                raise ValueError("centerline splines must share cubic knots")
+            ss = np.asarray(tr.err_ss, dtype=np.float64)
+            if not np.array_equal(ss, 0.5 * np.arange(len(ss))):
+                raise ValueError("lane table rows must be s = 0.5 * row (make_lane_width_lookup_table.py)")
+            tables = (tr.spline_x.t, tr.spline_x.c, tr.spline_y.c, tr.length, tr.err_left, tr.err_right)
+        else:
+            self.track = None
+        t, cx, cy, L, el, er = tables
+        t = np.ascontiguousarray(t, dtype=np.float64)
+        cx = np.ascontiguousarray(cx, dtype=np.float64)
+        cy = np.ascontiguousarray(cy, dtype=np.float64)
+        P = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)) if a is not None else None  # noqa: E731
+        el = None if el is None else np.ascontiguousarray(el, dtype=np.float64)
+        er = None if er is None else np.ascontiguousarray(er, dtype=np.float64)
+        nr = 0 if el is None else len(el)
         h = ctypes.c_void_p()
         self._check(self.lib.mr_track_create(ctypes.byref(h), int(device), P(t), len(t), P(cx), P(cy), len(cx),
-                                             float(tr.length), P(el), P(er), len(el)))
+                                             float(L), P(el), P(er), nr))
         self.h = h
-        self.length = float(tr.length)
+        self.length = float(L)
 
     def _check(self, rc):
         if rc != 0:
@@ -166,6 +175,8 @@ class DeviceTrack:
         if side not in lanes:
             if side not in ("right", "left"):
                 raise ValueError("side is 'right' or 'left'")
+            if self.track is None:
+                raise ValueError("lane tables need a named track (mpcracing.track.Track)")
             xy = self.track.right_lane_xy if side == "right" else self.track.left_lane_xy
             t, cx, cy, L = native_spline(self.lib, xy[:, 0], xy[:, 1], close_loop=False)
             P = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))  # noqa: E731

