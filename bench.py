@@ -3,19 +3,25 @@
 
 Workload (default ``--config C4``): BASELINE config 4, the blended-bicycle
 contouring MPC at N = 40 in fp32 on the Shanghai centerline, 8 192 synthetic
-instances per GPU (weak scaling: 8 GPUs = the 65 536-instance C4 batch).  One
-"step" = one batched solve of the rank's shard, inputs resident in HBM, outputs
-written to HBM (libmpcracing.so, one kernel launch).  Multi-GPU: one process per
-GPU, contiguous shards, no data-path collective; RCCL only gathers the counters.
+instances per GPU (weak scaling; the 8 shards of 8 192 union to the 65 536-instance
+C4 batch, mpcracing/workload.py).  One "step" = one batched solve of the rank's
+shard, inputs resident in HBM, outputs written to HBM (libmpcracing.so, one
+kernel launch).  Multi-GPU: one process per GPU, disjoint shards, no data-path
+collective; RCCL only reduces the counters.  ``--gpus N`` without a launcher
+(WORLD_SIZE unset) spawns the N rank processes itself before touching the GPU.
 
-Prints ONE JSON line (rank 0).  Also reports the roofline of the solve kernel
-against HBM (algorithmic bytes per SURVEY.md §8(d): 2*257*W*N bytes per
-instance-iteration plus (13N+31)*W bytes of per-solve I/O) and a CPU baseline
-(the oracle's dense IPM on a bounded sample, rank 0 / N=1 only).
+Prints ONE JSON line (rank 0), with the roofline of the solve kernel against HBM
+(algorithmic bytes per SURVEY.md §8(d): 2*257*W*N bytes per instance-iteration
+plus (13N+31)*W bytes of per-solve I/O) and the CPU baseline (rank 0, N = 1 only):
+the scalar C++ fp64 build of the same interior-point solver (mr_solver.h
+``Solver``, OpenMP over instances) on a time-bounded sample of the same shard.
 """
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -25,6 +31,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "mpc-racing_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+METRIC = "MPC solves/sec (batch, N=40) + p50 per-solve latency, 1/2/4/8 MI355X"
 
 
 def algorithmic_bytes(N, W, iters):
@@ -33,29 +40,69 @@ def algorithmic_bytes(N, W, iters):
     return float((2 * 257 * W * N * iters).sum() + iters.size * (13 * N + 31) * W)
 
 
-def cpu_baseline(name, budget_s):
-    """Oracle (dense IPM, numpy/torch autograd, fp64) on the first instances of the same shard."""
-    import torch
-    torch.set_num_threads(1)
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _cpu_threads():
+    avail = len(os.sched_getaffinity(0))
+    want = int(os.environ.get("OMP_NUM_THREADS", avail))
+    return max(1, min(avail, want))
+
+
+def cpu_baseline(name, batch, gpu_iters, budget_s):
+    """The scalar C++ fp64 IPM (libmpcracing_host.so ``mrh_solve_batch_scalar``: mr_solver.h Solver, the
+    same algorithm as the kernel, one instance per thread) on the host cores, on chunks of the rank's
+    shard until ``budget_s``; plus the single-instance latency of BASELINE.md §2 (C1 + 100 C2 instances,
+    one thread).  Termination: the fp64 defaults of the library (scaled KKT tol 1e-8, acceptable 1e-6
+    over 15 iterations)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import host_twin as ht
     from mpcracing import workload as wl
-    from oracle.nlp import MPCProblem, solve_ipm
     cfg = wl.CONFIGS[name]
-    b = wl.make_batch(name, limit=64)
+    cores = _cpu_threads()
     tyres = wl.tyre_coeffs(cfg["tyres"]) if cfg["tyres"] else None
+    c = ht.config(cfg["N"], cfg["model"], "fp64", cfg["lane"], cfg["Ts"], tol=1e-8, acceptable_iter=15,
+                  acceptable_tol=1e-6)
+    B = batch["s0"].shape[0]
+    chunk = 128 * cores
     n = 0
-    t0 = time.time()
-    for inst in wl.instance_dicts(b):
-        p = MPCProblem(inst["state0"], inst["s0"], inst["cx"], inst["cy"], inst["max_error"], N=cfg["N"],
-                       Ts=cfg["Ts"], model=cfg["model"], lane_bounds=cfg["lane"], tyres=tyres,
-                       elastic=1e5 if cfg["lane"] else None)
-        solve_ipm(p, tol=1e-8, max_iter=500)
-        n += 1
-        if time.time() - t0 > budget_s and n >= 2:
-            break
-    dt = time.time() - t0
-    return {"value": n / dt, "unit": "solves/s", "cores": 1, "kind": "port",
-            "sample": f"first {n} instances of the {name} shard, oracle dense primal-dual IPM "
-                      f"(fp64, tol 1e-8, single thread, {dt:.1f} s)"}
+    iters = []
+    t0 = time.perf_counter()
+    while n < B and time.perf_counter() - t0 < budget_s:
+        m = min(chunk, B - n)
+        sub = {k: (v[..., n:n + m].copy() if v is not None else None) for k, v in batch.items()}
+        o = ht.solve(c, sub, tyres=tyres, nthreads=cores, scalar=True)
+        iters.append(o["iters"])
+        n += m
+    dt = time.perf_counter() - t0
+    it = np.concatenate(iters)
+    # single-instance latency, one thread: C1 and 100 C2 instances
+    lat = []
+    c1 = wl.make_batch("C1")
+    k1 = ht.config(20, "kin", "fp64", False, 0.1, tol=1e-8, acceptable_iter=15, acceptable_tol=1e-6)
+    b2 = wl.make_batch("C2", limit=100)
+    k2 = ht.config(20, "kin", "fp64", False, 0.05, tol=1e-8, acceptable_iter=15, acceptable_tol=1e-6)
+    for kk, bb in [(k1, c1)] + [(k2, {k: (v[..., i:i + 1].copy() if v is not None else None)
+                                      for k, v in b2.items()}) for i in range(100)]:
+        t = time.perf_counter()
+        ht.solve(kk, bb, nthreads=1, scalar=True)
+        lat.append(time.perf_counter() - t)
+    lat = np.array(lat) * 1e3
+    return {"value": n / dt, "unit": "solves/s", "cores": cores, "kind": "port",
+            "sample": f"first {n} instances of this rank's {name} shard ({cfg['model']}, N={cfg['N']}), "
+                      f"scalar C++ fp64 build of the same IPM (mr_solver.h Solver, g++ -O2, OpenMP, "
+                      f"{cores} threads), tol 1e-8, {dt:.1f} s",
+            "cpu_model": _cpu_model(),
+            "iters_mean_cpu_fp64": float(it.mean()), "iters_mean_gpu_same_instances": float(gpu_iters[:n].mean()),
+            "latency_1core_ms": {"p50": float(np.median(lat)), "p90": float(np.quantile(lat, 0.9)),
+                                 "sample": "C1 + 100 C2 instances, one at a time, 1 thread"}}
 
 
 def reduce_counters(counts, elapsed, world):
@@ -72,6 +119,61 @@ def reduce_counters(counts, elapsed, world):
     return tot.cpu().numpy(), float(tmax.item())
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn(nproc, argv):
+    """One child process per rank (the launcher the driver would otherwise provide).  Runs before this
+    process touches the GPU; returns the worst exit code."""
+    port = str(_free_port())
+    procs = []
+    for r in range(nproc):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc), LOCAL_WORLD_SIZE=str(nproc),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    codes = [p.wait() for p in procs]
+    return max(abs(c) for c in codes)
+
+
+def _lib_sha():
+    from mpcracing import abi
+    h = hashlib.sha256()
+    with open(os.environ.get("MR_PRODUCT_LIB") or abi.PRODUCT_LIB, "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def cpu_check(args, rank, world):
+    """--cpu-check: the multi-rank plumbing without a GPU (gloo): each rank builds its shard and the
+    counters go through reduce_counters; rank 0 prints the shard layout.  Used by tests/test_multirank.py."""
+    import torch
+    import torch.distributed as dist
+    from mpcracing import workload as wl
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    per = args.per_gpu or wl.CONFIGS[args.config]["per_gpu"]
+    segs, K, n_shards = wl.shard_segments(args.config, rank, world, per)
+    b = wl.make_batch(args.config, rank=rank, world=world, per_gpu=per)
+    B = int(b["s0"].shape[0])
+    counts = torch.tensor([B, float(b["state0"][3].sum()), float(len(segs))], dtype=torch.float64)
+    tot, tmax = reduce_counters(counts, 1.0 + rank, world)
+    gathered = [None] * world
+    if world > 1:
+        dist.all_gather_object(gathered, segs)
+    else:
+        gathered = [segs]
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "instances": int(tot[0]), "vx_sum": float(tot[1]), "K": K,
+                          "n_shards": n_shards, "segments": gathered, "elapsed_max": tmax}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -79,19 +181,27 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="C4")
     ap.add_argument("--per-gpu", type=int, default=None)
-    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true", help="skip the B = 1 latency probe (profiling runs)")
+    ap.add_argument("--cpu-check", action="store_true", help="multi-rank plumbing on CPU (gloo), no solve")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn(args.gpus, sys.argv[1:]))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    if args.cpu_check:
+        return cpu_check(args, rank, world)
 
     import torch
     import torch.distributed as dist
     from mpcracing import workload as wl
     from mpcracing.batch import solver_for_config
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
@@ -114,9 +224,6 @@ def main():
 
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    iters_sum = 0.0
-    alg_bytes = 0.0
-    statuses = np.zeros(5, dtype=np.int64)
     W = 4 if cfg["precision"] == "fp32" else 8
     if world > 1:
         dist.barrier()
@@ -134,9 +241,8 @@ def main():
     kms = [starts[s].elapsed_time(ends[s]) for s in range(args.steps)]
     it = out["iters"].cpu().numpy()
     stc = np.bincount(out["status"].cpu().numpy(), minlength=5)[:5]
-    iters_sum = float(it.sum())
+    iters_launch = float(it.sum())            # one launch (every launch solves the same shard)
     alg_bytes = algorithmic_bytes(cfg["N"], W, it)
-    statuses += stc
 
     # B = 1 latency (same configuration, first instance), p50 of 5 runs
     lat_b1_ms = None
@@ -155,22 +261,24 @@ def main():
         lat_b1_ms = float(np.median(lat[1:]) * 1e3)
 
     tot, elapsed_max = reduce_counters(
-        torch.tensor([B * args.steps, iters_sum, alg_bytes] + statuses.tolist(), dtype=torch.float64, device=dev),
+        torch.tensor([B * args.steps, iters_launch, alg_bytes, B] + stc.tolist(), dtype=torch.float64, device=dev),
         elapsed, world)
 
     if rank == 0:
         solves = tot[0]
         kavg = float(np.mean(kms)) / 1e3
         achieved = alg_bytes / kavg / 1e9  # this rank's algorithmic bytes per launch / avg launch time
-        traffic = None
+        traffic, traffic_src = None, None
         pmc_path = os.path.join(REPO, "profiles", f"pmc_{args.config}.json")
         if os.path.exists(pmc_path):
             with open(pmc_path) as f:
                 pm = json.load(f)
-            if pm.get("B") == B:
+            if pm.get("B") == B and pm.get("lib_sha") == _lib_sha():
                 traffic = pm.get("hbm_bytes_per_launch")
+                traffic_src = (f"{os.path.relpath(pmc_path, REPO)}: rocprofv3 --pmc passes of this command on "
+                               f"the same libmpcracing.so build (sha {pm['lib_sha']})")
         line = {
-            "metric": "MPC solves/sec (batch, N=40) + p50 per-solve latency, 1/2/4/8 MI355X",
+            "metric": METRIC,
             "value": solves / elapsed_max,
             "unit": "solves/s",
             "n_gpus": world,
@@ -186,21 +294,19 @@ def main():
                                    f"{cfg['precision']}, {per} instances per GPU, track {cfg['track']}"
                                    + (", lane-bound rows" if cfg["lane"] else ""),
                        "config_id": args.config, "N": cfg["N"], "instances_per_gpu": per,
-                       "global_batch": int(per * world), "parallelism": f"dp{world} (instance shards)"},
+                       "global_batch": int(tot[3]), "parallelism": f"dp{world} (instance shards)"},
             "p50_batch_latency_ms": float(np.median(kms)),
             "p50_latency_b1_ms": lat_b1_ms,
-            "iters_mean": tot[1] / solves * args.steps / args.steps if solves else None,
-            "status_hist": {"solved": int(tot[3]), "acceptable": int(tot[4]), "max_iter": int(tot[5]),
-                            "failed": int(tot[6]), "lane_infeasible": int(tot[7])},
+            "iters_mean": float(tot[1] / tot[3]),
+            "status_hist": {"solved": int(tot[4]), "acceptable": int(tot[5]), "max_iter": int(tot[6]),
+                            "failed": int(tot[7]), "lane_infeasible": int(tot[8])},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "mr_wave_kernel", "avg_launch_ms": kavg * 1e3,
                          "alg_bytes_per_launch": alg_bytes},
         }
-        line["iters_mean"] = float(iters_sum / B)
         if world == 1 and not args.no_cpu_baseline:
-            sys.path.insert(0, REPO)
-            line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_budget)
+            line["cpu_baseline"] = cpu_baseline(args.config, batch, it, args.cpu_budget)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -50,6 +50,22 @@ static void run(const mr_config& c, const TyreCoef<double>& tf, const TyreCoef<d
   }
 }
 
+// The scalar C++ solver (mr_solver.h Solver: the same IPM, one instance per CPU thread, no wave
+// emulation) over a batch with OpenMP -- the CPU baseline that bench.py times beside the GPU
+// (SURVEY §8(d) "C++ fp64 CPU SQP twin").  Per-thread workspace of (N+1) stage records.
+template <typename T, int MODEL>
+static void run_scalar(const mr_config& c, const TyreCoef<double>& tf, const TyreCoef<double>& tr, int B,
+                       const mr_inputs& in, const mr_outputs& out, int nthreads) {
+  ProbParams<T> P;
+  fill_params<T>(c, tf, tr, P);
+#pragma omp parallel num_threads(nthreads > 0 ? nthreads : 1)
+  {
+    std::vector<T> ws((size_t)(c.N + 1) * WF::NF, (T)NAN);
+#pragma omp for schedule(dynamic, 1)
+    for (int i = 0; i < B; ++i) solve_instance<T, MODEL>(P, in, out, (int64_t)B, (int64_t)i, WS<T>{ws.data(), 1});
+  }
+}
+
 extern "C" {
 
 int mrh_config_default(mr_config* c) {
@@ -73,6 +89,19 @@ int mrh_solve_batch(const mr_config* c, const double* a_front, double Fz_front, 
     default: return -1;                                                    \
   }
   if (c->precision == MR_PREC_FP64) { MR_MODELS(double) } else { MR_MODELS(float) }
+#undef MR_CASE
+  return 0;
+}
+
+int mrh_solve_batch_scalar(const mr_config* c, const double* a_front, double Fz_front, const double* a_back,
+                           double Fz_back, int B, const mr_inputs* in, mr_outputs* out, int nthreads) {
+  TyreCoef<double> tf{}, tr{};
+  if (a_front) tf = pacejka_coef(a_front, Fz_front);
+  if (a_back) tr = pacejka_coef(a_back, Fz_back);
+  if (c->N < 1 || c->N > 63) return -1;
+#define MR_CASE(T, M) run_scalar<T, M>(*c, tf, tr, B, *in, *out, nthreads)
+  if (c->precision == MR_PREC_FP64) { MR_MODELS(double) } else { MR_MODELS(float) }
+#undef MR_CASE
   return 0;
 }
 

@@ -96,6 +96,7 @@ def load_host_twin(path=HOST_TWIN_LIB):
     lib.mrh_config_default.argtypes = [ctypes.POINTER(MRConfig)]
     lib.mrh_solve_batch.argtypes = [ctypes.POINTER(MRConfig), _PD, _D, _PD, _D, ctypes.c_int,
                                     ctypes.POINTER(MRInputs), ctypes.POINTER(MROutputs), ctypes.c_int]
+    lib.mrh_solve_batch_scalar.argtypes = lib.mrh_solve_batch.argtypes
     lib.mrh_eval_dynamics.argtypes = [ctypes.POINTER(MRConfig), _PD, _D, _PD, _D, _PD, _PD, _PD, _PD, _PD, _PD]
     lib.mrh_pacejka.argtypes = [_PD, _D, _D, ctypes.c_int, _PD]
     V, I = ctypes.c_void_p, ctypes.c_int

@@ -15,6 +15,14 @@ steer0 ~ U(-0.3, 0.3).  Fit window: lookback 5 m, lookahead N*Ts*v_max + 25 m
 (ParameterizedLine.x_as_coeffs, deg 4).  Segment k draws from
 numpy.random.default_rng([1000 + config#, k]) so any shard of the batch is
 reproducible independently of the number of GPUs.
+
+Sharding (SURVEY §8(e), weak scaling): the global batch of a config is fixed --
+K segments in lap order x M states (C4: 512 x 128 = 65 536).  It splits into
+``n_shards = B / per_gpu`` disjoint shards of per_gpu instances (C4: 8 x 8 192);
+shard r holds segments r, r + n_shards, r + 2 n_shards, ... so every shard spans
+the whole lap (the same instance mix, hence balanced ranks).  Rank r of a world of
+W <= n_shards GPUs solves shard r: the 1-GPU bench line is rank 0's shard of the
+8-GPU run, and the 8 shards union to the full batch.
 """
 import json
 import os
@@ -94,20 +102,36 @@ def config1_instance():
     return dict(state0=st, s0=np.array([s0]), cx=cx[:, None], cy=cy[:, None], max_error=np.array([max_err]))
 
 
+def shard_segments(name, rank=0, world=1, per_gpu=None):
+    """(segment indices of ``rank``'s shard, K total segments, n_shards) -- see the module doc."""
+    cfg = CONFIGS[name]
+    M = cfg["M"]
+    per = per_gpu or cfg["per_gpu"]
+    if per % M:
+        raise ValueError(f"per_gpu ({per}) must be a multiple of M = {M} states per segment")
+    n_shards = max(1, cfg["B"] // per)
+    if world > n_shards:
+        raise ValueError(f"{name}: {world} ranks but only {n_shards} shards of {per} instances "
+                         f"(global batch {cfg['B']}); lower per_gpu")
+    if not 0 <= rank < world:
+        raise ValueError("rank out of range")
+    K = n_shards * (per // M)
+    return list(range(rank, K, n_shards)), K, n_shards
+
+
 def make_batch(name, rank=0, world=1, per_gpu=None, limit=None):
     """The shard of config ``name`` owned by ``rank`` (weak scaling: per_gpu instances per rank)."""
     cfg = CONFIGS[name]
     if name == "C1":
+        if world != 1:
+            raise ValueError("C1 is a single instance")
         parts = [config1_instance()]
     else:
         M = cfg["M"]
-        per = per_gpu or cfg["per_gpu"]
-        B_tot = per * world
-        K = max(1, B_tot // M)
-        k_lo, k_hi = rank * K // world, (rank + 1) * K // world
+        segs, K, _ = shard_segments(name, rank, world, per_gpu)
         if limit is not None:
-            k_hi = min(k_hi, k_lo + max(1, -(-limit // M)))
-        parts = [segment_instances(cfg, k, K, M) for k in range(k_lo, k_hi)]
+            segs = segs[:max(1, -(-limit // M))]
+        parts = [segment_instances(cfg, k, K, M) for k in segs]
     b = {key: np.concatenate([p[key] for p in parts], axis=-1) for key in parts[0]}
     if limit is not None:
         b = {key: v[..., :limit] for key, v in b.items()}

@@ -16,12 +16,15 @@ step() {  # name limit cmd...
 }
 what=${1:-all}
 if [ "$what" = all ] || [ "$what" = tests ]; then
-  step pytest_gpu 1200 python -m pytest tests -m gpu -q -rA
+  step pytest_gpu 1100 python -u -m pytest tests -m gpu -v -rA --timeout 300 --timeout-method thread
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [ "$what" = all ] || [ "$what" = bench ]; then
   step bench 900 python bench.py
   step prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline
+fi
+if [ "$what" = probe ]; then
+  step fp32_probe 600 python -u mpc-racing_amd/tools/fp32_probe.py 256 4
 fi
 if [ "$what" = pmc ]; then
   step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline

@@ -44,8 +44,9 @@ def _p(a):
     return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
 
 
-def solve(cfg, batch, tyres=None, nthreads=8, trace_instance=-1, trace_cap=0):
-    """batch: dict of numpy arrays in ABI layout (see include/mpcracing.h)."""
+def solve(cfg, batch, tyres=None, nthreads=8, trace_instance=-1, trace_cap=0, scalar=False):
+    """batch: dict of numpy arrays in ABI layout (see include/mpcracing.h).  scalar=True runs the
+    scalar C++ solver (mr_solver.h Solver, the CPU baseline) instead of the emulated wave."""
     N = cfg.N
     B = batch["s0"].shape[0]
     arr = {k: np.ascontiguousarray(v, dtype=np.float64) for k, v in batch.items() if v is not None}
@@ -67,6 +68,7 @@ def solve(cfg, batch, tyres=None, nthreads=8, trace_instance=-1, trace_cap=0):
     else:
         pa = pb = None
         Fzf = Fzr = 0.0
-    rc = lib().mrh_solve_batch(ctypes.byref(cfg), pa, Fzf, pb, Fzr, B, ctypes.byref(inp), ctypes.byref(o), nthreads)
+    fn = lib().mrh_solve_batch_scalar if scalar else lib().mrh_solve_batch
+    rc = fn(ctypes.byref(cfg), pa, Fzf, pb, Fzr, B, ctypes.byref(inp), ctypes.byref(o), nthreads)
     assert rc == 0
     return out

@@ -1,11 +1,12 @@
 """GPU parity tests of libmpcracing.so (gfx950) through its C ABI.
 
-Parity tolerances: fp64 solves at KKT tol 1e-10 match the
-oracle's NLP solution to 1e-6 in controls, states, progress and errors, except
+Parity tolerances: fp64 solves at KKT tol 1e-10 match the oracle's
+NLP solution (itself pinned to the reference's MPC.__init__, tests/test_nlp_golden.py)
+to 1e-6 in controls, states (terminal column included), progress and errors, except
 the last throttle U[0, N-1] (it only reaches the cost through
-exp(q_v_max (vx_N - v_max)) ~ e^-60, so only the barrier fixes it) and the state
-it drives, vx_N.  fp32 solves are checked against fp64 with stated looser bounds
-and by full-batch feasibility properties.
+exp(q_v_max (vx_N - v_max)) ~ e^-60, so only the barrier fixes it) and the one
+state it drives, vx_N.  fp32 solves are checked against fp64 and the oracle with
+the bounds derived in DESIGN.md §4 and by full-batch feasibility properties.
 """
 import math
 
@@ -35,7 +36,9 @@ def _parity(cfg, inst, o, i, tyres=None, parity=1e-6):
     dU = np.abs(U - o["U"][:, :, i])
     dU[0, -1] = 0.0
     assert dU.max() < parity, dU.max()
-    assert np.abs(X[:, :-1] - o["X"][:, :-1, i]).max() < parity
+    dX = np.abs(X - o["X"][:, :, i])
+    dX[3, -1] = 0.0  # vx_N: driven only by U[0, N-1]
+    assert dX.max() < parity, dX.max()
     assert np.abs(S - o["S"][:, i]).max() < parity
     assert np.abs(eC - o["eC"][:, i]).max() < parity and np.abs(eL - o["eL"][:, i]).max() < parity
     assert abs(r.obj - o["obj"][i]) <= 1e-8 * max(1.0, abs(r.obj))

@@ -124,7 +124,6 @@ def test_dropin_line_from_waypoints():
     p = "t4/"
     assert np.array_equal(cl.spline_x.t, G[p + "t"])
     s = np.linspace(-10, cl.length + 10, 97)
-    assert np.array_equal(cl.Gx(s), G[p + "g2_vals"][:0, 0]) or True
     h = cl.host_track
     np.testing.assert_allclose(cl.Gx(s), h.Gx(s), rtol=0, atol=1e-12)
     np.testing.assert_allclose(cl.dGy(s), h.dGy(s), rtol=0, atol=1e-12)

@@ -1,63 +1,54 @@
-"""Multi-rank path of bench.py on CPU (gloo, world_size 2): contiguous instance shards per rank
-with no data-path collective, and the one counter all-reduce (SUM) / wall-clock max of the run.
-The same code runs over RCCL ("nccl") with one process per MI355X on the GPU box."""
+"""Multi-rank path of bench.py on CPU (gloo): ``bench.py --gpus 2`` spawns its two rank processes itself
+(WORLD_SIZE unset, the driver's plain invocation), each builds its shard, and the counters go through
+the real ``reduce_counters`` (the run's only collective; RCCL "nccl" on the GPU box).  Checks: the
+right number of ranks, disjoint shards that span the lap and union to the config's batch, and the
+reduced totals."""
+import json
 import os
-import socket
+import subprocess
 import sys
 
 import numpy as np
 import pytest
-import torch
-import torch.distributed as dist
-import torch.multiprocessing as mp
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def _run(*argv):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *argv, "--cpu-check"], env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
 
 
-def _rank_main(rank, world, port, per, q):
-    sys.path.insert(0, REPO)
-    sys.path.insert(0, os.path.join(REPO, "mpc-racing_amd"))
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    import bench
-    from mpcracing import workload as wl
-    b = wl.make_batch("C4", rank=rank, world=world, per_gpu=per)
-    B = b["s0"].shape[0]
-    # stand-in per-rank counters (the GPU solve is not run here): instances, a checksum of the
-    # shard, and a status histogram
-    counts = torch.tensor([B, float(b["state0"][3].sum()), 0.0, B, 0, 0, 0, 0], dtype=torch.float64)
-    tot, tmax = bench.reduce_counters(counts, elapsed=1.0 + rank, world=world)
-    q.put((rank, b["s0"].tolist(), tot.tolist(), tmax))
-    dist.destroy_process_group()
-
-
-@pytest.mark.parametrize("world", [2])
-def test_shards_and_counter_reduce(world):
+@pytest.mark.parametrize("world", [2, 4])
+def test_spawned_ranks_shard_the_batch(world):
     per = 256
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, per, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = sorted(q.get(timeout=120) for _ in range(world))
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    out = _run("--gpus", str(world), "--config", "C4", "--per-gpu", str(per))
+    assert out["n_gpus"] == world and out["instances"] == per * world
+    segs = out["segments"]
+    assert len(segs) == world
+    flat = [k for s in segs for k in s]
+    assert len(flat) == len(set(flat))                        # disjoint
+    n_shards = out["n_shards"]
+    assert n_shards == 65536 // per and out["K"] == n_shards * (per // 128)
+    for r, s in enumerate(segs):
+        assert s == list(range(r, out["K"], n_shards))        # every shard spans the lap
+    assert out["elapsed_max"] == float(world)                  # max over ranks of 1 + rank
     sys.path.insert(0, os.path.join(REPO, "mpc-racing_amd"))
     from mpcracing import workload as wl
-    full = wl.make_batch("C4", rank=0, world=1, per_gpu=per * world)
-    # the shards are contiguous and partition the weak-scaled batch exactly
-    assert np.array_equal(np.concatenate([np.asarray(r[1]) for r in res]), full["s0"])
-    for _, _, tot, tmax in res:
-        assert tot[0] == per * world and tot[3] == per * world
-        assert abs(tot[1] - full["state0"][3].sum()) < 1e-6 * abs(full["state0"][3].sum())
-        assert tmax == float(world)  # max over ranks of 1 + rank
+    tot = sum(float(wl.make_batch("C4", rank=r, world=world, per_gpu=per)["state0"][3].sum()) for r in range(world))
+    assert abs(out["vx_sum"] - tot) <= 1e-9 * tot
+
+
+def test_single_rank_is_rank0_of_eight():
+    """The 1-GPU bench shard is rank 0's shard of the 8-GPU run (same instances)."""
+    sys.path.insert(0, os.path.join(REPO, "mpc-racing_amd"))
+    from mpcracing import workload as wl
+    a = wl.make_batch("C4", rank=0, world=1, per_gpu=1024)
+    b = wl.make_batch("C4", rank=0, world=8, per_gpu=1024)
+    for k in ("state0", "s0", "cx", "cy", "max_error"):
+        assert np.array_equal(a[k], b[k])
+    with pytest.raises(ValueError):
+        wl.make_batch("C4", rank=0, world=128, per_gpu=1024)  # more ranks than shards

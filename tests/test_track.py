@@ -37,8 +37,16 @@ def test_queries(track):
 
 
 def test_workload_shards_partition_the_batch():
+    """The n_shards strided shards of a config are disjoint and union to its global batch (C4 at 1 024 per
+    shard: 64 shards of 8 segments; the full batch = all 512 segments in lap order)."""
     from mpcracing import workload as wl
-    full = wl.make_batch("C2", rank=0, world=1, per_gpu=256)
-    parts = [wl.make_batch("C2", rank=r, world=4, per_gpu=64) for r in range(4)]
-    for k in ("state0", "s0", "cx", "cy", "max_error"):
-        assert np.array_equal(np.concatenate([p[k] for p in parts], axis=-1), full[k])
+    full = wl.make_batch("C4", rank=0, world=1, per_gpu=65536, limit=None)
+    M = wl.CONFIGS["C4"]["M"]
+    n = 8
+    for r in range(n):
+        part = wl.make_batch("C4", rank=r, world=n, per_gpu=8192)
+        segs, K, n_shards = wl.shard_segments("C4", r, n, 8192)
+        assert K == 512 and n_shards == 8 and segs == list(range(r, 512, 8))
+        cols = np.concatenate([np.arange(k * M, (k + 1) * M) for k in segs])
+        for k in ("state0", "s0", "cx", "cy", "max_error"):
+            assert np.array_equal(part[k], full[k][..., cols])
