@@ -21,7 +21,7 @@ if [ "$what" = all ] || [ "$what" = tests ]; then
 fi
 if [ "$what" = all ] || [ "$what" = bench ]; then
   step bench 900 python bench.py
-  step prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline
+  step prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-latency
 fi
 if [ "$what" = probe ]; then
   step fp32_probe 600 python -u mpc-racing_amd/tools/fp32_probe.py 256 4

@@ -80,9 +80,16 @@ def test_c2_full_batch_matches_host_build():
     assert dU.max() < 1e-6
 
 
-def _defects(cfg, o, ok):
+def _defects(cfg, o, ok, tyres=None):
     """Dynamics residual F(X_k, U_k) - X_{k+1} of the returned trajectories (oracle dynamics, fp64)."""
     f = dyn.model_fn(cfg["model"])
+    fns = None
+    if tyres is not None:
+        from oracle.nlp import pacejka_torch
+        import torch as _t
+        pf, pr = (pacejka_torch(a, Fz) for a, Fz in tyres)
+        fns = (lambda al: float(pf(_t.tensor(float(al), dtype=_t.float64))) if al != 0 else 0.0,
+               lambda al: float(pr(_t.tensor(float(al), dtype=_t.float64))) if al != 0 else 0.0)
     N = cfg["N"]
     X = o["X"][:, :, ok]
     U = o["U"][:, :, ok]
@@ -93,8 +100,8 @@ def _defects(cfg, o, ok):
         if cfg["model"] in ("kin", "dyn"):
             fk = f(x, u, cfg["Ts"])
         else:  # blended law per instance
-            fk = np.stack([dyn.f_blend([X[j, k, i] for j in range(6)], [U[0, k, i], U[1, k, i]], cfg["Ts"])
-                           for i in range(X.shape[2])], axis=1)
+            fk = np.stack([dyn.f_blend([X[j, k, i] for j in range(6)], [U[0, k, i], U[1, k, i]], cfg["Ts"],
+                                       tyres=fns) for i in range(X.shape[2])], axis=1)
         worst = max(worst, float(np.abs(fk - X[:, k + 1]).max()))
     return worst
 
@@ -142,15 +149,49 @@ def test_c3_full_batch_lane_rows():
     assert _defects(cfg, {k: v[..., :256] for k, v in o.items()}, ok[:256]) < 1e-7
 
 
-def test_fp32_vs_fp64_same_instances():
-    b = wl.make_batch("C4", limit=256)
-    s64 = BatchSolver(40, "blend", "fp64", max_batch=256)
-    s32 = BatchSolver(40, "blend", "fp32", max_batch=256)
-    o64, o32 = _np(s64.solve(b)), _np(s32.solve(b))
-    ok = (o64["status"] <= 1) & (o32["status"] <= 1)
-    assert ok.mean() > 0.9
-    dU = np.abs(o64["U"] - o32["U"])[:, :-1, ok]
-    assert np.median(dU) < 1e-3 and np.quantile(dU, 0.99) < 5e-2
+@pytest.mark.parametrize("name", ["C4", "C5"])
+def test_fp32_accuracy_vs_reference_tolerance(name):
+    """fp32 (the benchmarked precision) against the exact fp64 optimum (tol 1e-10), measured against what
+    the reference's own termination leaves: an fp64 solve with IPOPT's options of control/MPC.py:152-161
+    (tol 1e-4, acceptable_tol 1e-2 over 15 iterations), which the fp32 solve also uses.  Bar (DESIGN.md
+    §4): fp32 rounding adds essentially nothing beyond that tolerance -- per instance the control error
+    of fp32 is within 1.5x (+1e-3) of the fp64-at-reference-tolerance error for >= 95 % of the
+    instances, and the median / 99th-percentile relative objective gap is within 1.5x (+1e-6) of it."""
+    cfg = wl.CONFIGS[name]
+    tyres = wl.tyre_coeffs(cfg["tyres"]) if cfg["tyres"] else None
+    n = 512
+    b = wl.make_batch(name, limit=n)
+    mk = lambda prec, **kw: BatchSolver(cfg["N"], cfg["model"], prec, max_batch=n, tyres=tyres, **kw)  # noqa: E731
+    o64 = _np(mk("fp64", tol=1e-10, acceptable_iter=0).solve(b))
+    o32 = _np(mk("fp32").solve(b))
+    oref = _np(mk("fp64", tol=1e-4, acceptable_tol=1e-2, acceptable_iter=15).solve(b))
+    ok = (o64["status"] == 0) & (o32["status"] <= 1) & (oref["status"] <= 1)
+    assert ok.mean() >= 0.97, (np.bincount(o64["status"]), np.bincount(o32["status"]))
+    d32 = np.abs(o64["U"] - o32["U"])[:, :-1, ok].max(axis=(0, 1))
+    dref = np.abs(o64["U"] - oref["U"])[:, :-1, ok].max(axis=(0, 1))
+    assert (d32 <= 1.5 * dref + 1e-3).mean() >= 0.95, np.quantile(d32 / np.maximum(dref, 1e-6), [0.5, 0.9, 0.99])
+    loc = lambda o: (o["obj"] + 300.0 * b["s0"])[ok]  # noqa: E731  (local objective, -lambda_s s0 removed)
+    g32 = (loc(o32) - loc(o64)) / np.abs(loc(o64))
+    gref = (loc(oref) - loc(o64)) / np.abs(loc(o64))
+    for q in (0.5, 0.99):
+        assert np.quantile(g32, q) <= 1.5 * np.quantile(gref, q) + 1e-6, (q, np.quantile(g32, q), np.quantile(gref, q))
+    assert np.median(g32) < 1e-4  # the objective itself: median within 1e-4 of the optimum
+
+
+def test_c5_full_batch_fp32_properties():
+    """C5 (blended + learned Pacejka, N = 60, fp32, the 16 384-instance shard): statuses, feasibility of every
+    row, dynamics defects of the returned trajectories against the oracle's fp64 model (pacejka-2 tyres)."""
+    cfg = wl.CONFIGS["C5"]
+    tyres = wl.tyre_coeffs(cfg["tyres"])
+    b = wl.make_batch("C5")
+    assert b["s0"].shape[0] == 16384
+    s = solver_for_config("C5", 16384)
+    o = _np(s.solve(b))
+    ok = o["status"] <= 1
+    assert ok.mean() >= 0.95, np.bincount(o["status"], minlength=5)
+    _check_feasible(cfg, o, o["status"] == 0, 1e-3)
+    _check_feasible(cfg, o, ok, 1e-2)
+    assert _defects(cfg, {k: v[..., :256] for k, v in o.items()}, ok[:256], tyres=tyres) < 5e-3
 
 
 def test_dropin_mpc_class():
