@@ -108,6 +108,13 @@ typedef struct mr_outputs {
                       kkt, mu, alpha_primal, alpha_dual, delta (inertia), theta, phi, line-search trials */
   int32_t trace_instance;
   int32_t trace_cap;
+  double* lam_g;   /* optional [13N+9][B]: the reference's dual = sol.value(opti.lam_g) (control/MPC.py:171)
+                      in Opti row order (MPC.py:101-149): S_0, X_{:,0} (6), per i = 1..N the 6 dynamics rows and
+                      the Delta-S row, per i = 0..N-1 thr < d_max, thr > min, steer < max, steer > min, the
+                      throttle and steer rate rows (i = 0: against U[:, N-1]), then the state0 throttle and
+                      steer rows (NaN when state0 has no throttle / steer).  CasADi convention: Lagrangian
+                      f + lam_g . g, canonical row = the non-constant side (positive at an active upper
+                      bound); unscaled objective.  NULL to skip. */
 } mr_outputs;
 
 typedef struct mr_handle mr_handle;

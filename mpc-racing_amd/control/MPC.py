@@ -11,8 +11,9 @@ Differences that are visible to a caller:
   * ``sol`` is a ``SolveInfo`` record (truthy) instead of a CasADi OptiSol; it is
     ``None`` when the solve did not converge, as in the reference's except branch
     (:172-181) -- but no ``breakpoint()`` is hit and ``ret`` holds the last iterate.
-  * ``dual`` is ``None`` (the reference returns Opti's lam_g; callers only feed it
-    back as the ignored ``duals`` argument).
+  * ``dual`` is the reference's ``opti.lam_g`` (MPC.py:171): one multiplier per
+    constraint row in Opti order, CasADi's sign convention (include/mpcracing.h
+    ``lam_g``); ``None`` on failure, as the reference.
   * the solver is a primal-dual interior-point method with IPOPT's rules, run to
     tol 1e-8 (the reference's IPOPT tol is 1e-4).
 """
@@ -110,7 +111,7 @@ class MPC:
             u_init=u_init,
         )
         solver = get_solver(N, Ts, model, lane_bounds, device=device)
-        out = {k: v.cpu().numpy() for k, v in solver.solve(batch).items()}
+        out = {k: v.cpu().numpy() for k, v in solver.solve(batch, duals=True).items()}
         status = int(out["status"][0])
         from mpcracing.abi import STATUS
         info = SolveInfo(STATUS.get(status, str(status)), int(out["iters"][0]), float(out["obj"][0]),
@@ -118,12 +119,14 @@ class MPC:
         self.info = info
         self.ret = (out["X"][:, :, 0], out["U"][:, :, 0], out["S"][:, 0],
                     [float(v) for v in out["eC"][:, 0]], [float(v) for v in out["eL"][:, 0]])
+        lam = out["lam_g"][:, 0]
         if status in (0, 1):
             self.sol = info
+            self.dual = lam[~np.isnan(lam)]  # state0 rows absent when its throttle / steer is None
         else:
             print(f"MPC solve did not converge: {info.status} after {info.iterations} iterations")
             self.sol = None
-        self.dual = None
+            self.dual = None
 
     def solution(self):
         return self.sol, self.ret, self.dual

@@ -1120,6 +1120,55 @@ MR_HD void solve_instance_wave(const ProbParams<T>& P, const mr_inputs& in, cons
   }
 }
 
+// The reference's dual (control/MPC.py:171: sol.value(opti.lam_g)) from the stage-wise multipliers, in
+// Opti row order (include/mpcracing.h lam_g).  Derivation: the solver's Lagrangian is
+// sc*f + sum nu_{k+1}.(F(x_k, u_k) - x_{k+1}) - sum lam.d, Opti's is f + lam_g.g with g = X_i - f(X_{i-1},
+// U_{i-1}), so the dynamics rows are -nu/sc; every inequality row of the reference is a row of the
+// restatement (Delta-S = the u[2] box, rate rows via the previous-control state p, the i = 0 wrap rows via
+// the frozen copy w at k = N-1), lam_g = (lam_upper - lam_lower)/sc; S_0 and X_{:,0} follow from the
+// reference's stationarity in those variables: lam_S0 = lam_ds(1), lam_X0 = A_0^T lam_dyn(1).
+template <typename Solver>
+MR_HD void write_lam_g(Solver& S, const mr_outputs& out, int64_t B, int64_t i, int N, Wv w) {
+  typedef decltype(S.mu) T;
+  const int k = w.lane;
+  const double isc = 1.0 / (double)S.sc;
+  const int rows = 13 * N + 9;
+  auto put = [&](int row, double v) { out.lam_g[(int64_t)row * B + i] = v; };
+  auto lam = [&](int j) { return (double)S.S(SSF::LAM + j); };
+  T nu1[NX];
+  for (int q = 0; q < NX; ++q) nu1[q] = wshfl(w, S.own() ? S.S(SSF::NU + q) : T(0), 1);
+  const double ds1 = wshfl(w, S.own() && k < N ? (lam(5) - lam(4)) * isc : 0.0, 0);
+  if (k >= 1 && k <= N)
+    for (int q = 0; q < 6; ++q) put(7 + 7 * (k - 1) + q, -(double)S.S(SSF::NU + q) * isc);
+  if (k < N) {
+    put(7 + 7 * k + 6, (lam(5) - lam(4)) * isc);  // Delta-S row of i = k + 1 (u[2] box of stage k)
+    const int b = 7 + 7 * N + 6 * k;
+    put(b + 0, lam(1) * isc);    // U[0,k] < d_max
+    put(b + 1, -lam(0) * isc);   // U[0,k] > min_throttle
+    put(b + 2, lam(3) * isc);    // U[1,k] < max_steer
+    put(b + 3, -lam(2) * isc);   // U[1,k] > min_steer
+    if (k >= 1) {
+      put(b + 4, (lam(7) - lam(6)) * isc);
+      put(b + 5, (lam(9) - lam(8)) * isc);
+    }
+    if (k == N - 1) {  // i = 0 rate rows U[:,0] - U[:,N-1]: the frozen-copy rows at stage N-1
+      const int b0 = 7 + 7 * N;
+      put(b0 + 4, N >= 2 ? (lam(11) - lam(10)) * isc : 0.0);
+      put(b0 + 5, N >= 2 ? (lam(13) - lam(12)) * isc : 0.0);
+    }
+  }
+  if (k == 0) {
+    put(0, ds1);  // S_0 == s0
+    MR_GLOBAL T* R0 = S.R(0);
+    T J[48], at[NX];
+    for (int q = 0; q < 48; ++q) J[q] = R0[RCF::J + q];
+    apply_At(J, 0, nu1, at);
+    for (int q = 0; q < 6; ++q) put(1 + q, -(double)at[q] * isc);  // X_{q,0} == state0
+    put(rows - 2, S.I.has_thr0 ? (lam(7) - lam(6)) * isc : NAN);
+    put(rows - 1, S.I.has_steer0 ? (lam(9) - lam(8)) * isc : NAN);
+  }
+}
+
 template <typename Solver>
 MR_HD void run_instance(Solver& S, const mr_inputs& in, const mr_outputs& out, int64_t B, int64_t i, int N,
                         double X0, double Y0, double s0, Wv w) {
@@ -1148,6 +1197,7 @@ MR_HD void run_instance(Solver& S, const mr_inputs& in, const mr_outputs& out, i
       out.eL[k * B + i] = (double)e.eL;
     }
   }
+  if (out.lam_g) write_lam_g(S, out, B, i, N, w);
   if (P.lane && (r.status == 0 || r.status == 1) && (double)viol > 1e-6) r.status = MR_STATUS_LANE_INFEASIBLE;
   if (w.lane == 0) {
     out.status[i] = r.status;

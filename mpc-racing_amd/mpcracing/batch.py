@@ -76,14 +76,18 @@ class BatchSolver:
                 out[k] = torch.from_numpy(np.ascontiguousarray(v, dtype=np.float64)).to(self.device)
         return out
 
-    def alloc_outputs(self, B):
+    def alloc_outputs(self, B, duals=False):
+        """Output tensors; ``duals`` adds ``lam_g`` [13N+9][B] (the reference's opti.lam_g, Opti row order)."""
         N, d = self.N, self.device
         f = dict(dtype=torch.float64, device=d)
-        return {"X": torch.empty((6, N + 1, B), **f), "U": torch.empty((2, N, B), **f),
-                "S": torch.empty((N + 1, B), **f), "eC": torch.empty((N, B), **f), "eL": torch.empty((N, B), **f),
-                "status": torch.empty(B, dtype=torch.int32, device=d),
-                "iters": torch.empty(B, dtype=torch.int32, device=d),
-                "obj": torch.empty(B, **f), "kkt": torch.empty(B, **f)}
+        out = {"X": torch.empty((6, N + 1, B), **f), "U": torch.empty((2, N, B), **f),
+               "S": torch.empty((N + 1, B), **f), "eC": torch.empty((N, B), **f), "eL": torch.empty((N, B), **f),
+               "status": torch.empty(B, dtype=torch.int32, device=d),
+               "iters": torch.empty(B, dtype=torch.int32, device=d),
+               "obj": torch.empty(B, **f), "kkt": torch.empty(B, **f)}
+        if duals:
+            out["lam_g"] = torch.empty((13 * N + 9, B), **f)
+        return out
 
     def launch(self, dev_in, out, stream=None, trace_instance=-1):
         """Enqueue one batched solve on ``stream`` (default: torch's current stream); no sync."""
@@ -103,16 +107,16 @@ class BatchSolver:
         tr = out.get("trace")
         o = abi.MROutputs(*[ptr(out.get(k)) for k in ("X", "U", "S", "eC", "eL", "status", "iters", "obj", "kkt",
                                                       "trace")], int(trace_instance),
-                          int(tr.shape[0]) if tr is not None else 0)
+                          int(tr.shape[0]) if tr is not None else 0, ptr(out.get("lam_g")))
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
         self._check(self.lib.mr_solve_batch(self.h, B, ctypes.byref(inp), ctypes.byref(o),
                                             ctypes.c_void_p(st.cuda_stream)))
         return out
 
-    def solve(self, batch, stream=None, trace_instance=-1, trace_cap=0):
+    def solve(self, batch, stream=None, trace_instance=-1, trace_cap=0, duals=False):
         """Blocking solve of a host or device batch; returns device output tensors."""
         dev_in = self.to_device(batch)
-        out = self.alloc_outputs(int(dev_in["s0"].shape[0]))
+        out = self.alloc_outputs(int(dev_in["s0"].shape[0]), duals=duals)
         if trace_cap:
             out["trace"] = torch.zeros((trace_cap, 8), dtype=torch.float64, device=self.device)
         self.launch(dev_in, out, stream, trace_instance)

@@ -24,7 +24,7 @@ def build_hip(force=False, verbose=True, out=None, flags=None):
     """Build libmpcracing.so (or a developer A/B variant at ``out`` with ``flags`` replacing the
     default code-generation flags; load it with MR_PRODUCT_LIB)."""
     out = out or PRODUCT_LIB
-    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(INCLUDE, "mpcracing.h")]
+    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(INCLUDE, "mpcracing.h"), __file__]
     if not force and not _stale(out, deps):
         return out
     # FMA contraction on (-ffp-contract=fast): the round-1 note about "huge defects at iteration 0" with

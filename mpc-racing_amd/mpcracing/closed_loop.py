@@ -93,8 +93,15 @@ class ClosedLoop:
 
     # ------------------------------------------------------------------ one tick
     def tick(self, stream=None):
-        """agent.run_step for every vehicle; returns this tick's record (device tensors, no sync)."""
+        """agent.run_step for every vehicle; returns this tick's record (device tensors, no sync).
+        Everything -- the library launches and the torch glue between them -- is ordered on ``stream``
+        (torch's current stream by default), so the caching allocator and the clones see the kernels'
+        order."""
         st = stream if stream is not None else torch.cuda.current_stream(self.dev)
+        with torch.cuda.stream(st):
+            return self._tick(st)
+
+    def _tick(self, st):
         sp = ctypes_stream(st)
         B, s = self.B, self.state
         X, Y, yaw, vx, vy = s[0], s[1], s[2], s[3], s[4]

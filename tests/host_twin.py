@@ -44,7 +44,7 @@ def _p(a):
     return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
 
 
-def solve(cfg, batch, tyres=None, nthreads=8, trace_instance=-1, trace_cap=0, scalar=False):
+def solve(cfg, batch, tyres=None, nthreads=8, trace_instance=-1, trace_cap=0, scalar=False, duals=False):
     """batch: dict of numpy arrays in ABI layout (see include/mpcracing.h).  scalar=True runs the
     scalar C++ solver (mr_solver.h Solver, the CPU baseline) instead of the emulated wave."""
     N = cfg.N
@@ -57,8 +57,10 @@ def solve(cfg, batch, tyres=None, nthreads=8, trace_instance=-1, trace_cap=0, sc
            "iters": np.zeros(B, np.int32), "obj": np.zeros(B), "kkt": np.zeros(B)}
     if trace_cap:
         out["trace"] = np.zeros((trace_cap, 8))
+    if duals:
+        out["lam_g"] = np.zeros((13 * N + 9, B))
     o = abi.MROutputs(*[_p(out.get(k)) for k in ("X", "U", "S", "eC", "eL", "status", "iters", "obj", "kkt",
-                                                 "trace")], trace_instance, trace_cap)
+                                                 "trace")], trace_instance, trace_cap, _p(out.get("lam_g")))
     if tyres is not None:
         (af, Fzf), (ar, Fzr) = tyres
         af = np.asarray(af, np.float64)

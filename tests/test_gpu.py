@@ -203,7 +203,7 @@ def test_dropin_mpc_class():
     m = MPC(st, 69.6, c["cx"][:, 0].tolist(), c["cy"][:, 0].tolist(), float(c["max_error"][0]),
             RuntimeControllerParameters(), Ts=0.1, N=20)
     sol, ret, dual = m.solution()
-    assert sol and dual is None
+    assert sol and dual.shape == (13 * 20 + 9,)
     States, U, S_hat, eC, eL = ret
     assert States.shape == (6, 21) and U.shape == (2, 20) and S_hat.shape == (21,)
     assert len(eC) == 20 and len(eL) == 20 and math.isclose(S_hat[0], 69.6)
