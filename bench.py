@@ -185,6 +185,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true", help="skip the B = 1 latency probe (profiling runs)")
     ap.add_argument("--cpu-check", action="store_true", help="multi-rank plumbing on CPU (gloo), no solve")
+    ap.add_argument("--dispatch-order", type=int, default=1, help="mr_config.dispatch_order (A/B runs)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -213,7 +214,7 @@ def main():
     per = args.per_gpu or cfg["per_gpu"]
     batch = wl.make_batch(args.config, rank=rank, world=world, per_gpu=per)
     B = int(batch["s0"].shape[0])
-    solver = solver_for_config(args.config, B, device=local)
+    solver = solver_for_config(args.config, B, device=local, dispatch_order=args.dispatch_order)
     dev_in = solver.to_device(batch)
     out = solver.alloc_outputs(B)
     stream = torch.cuda.current_stream(dev)

@@ -79,6 +79,11 @@ typedef struct mr_config {
   /* VehicleParameters (models/VehicleParameters.py:3-41); max_steer_deg = VehicleParameters.max_steer */
   double m, Iz, lf, lr, Cf, Cr, T_max, r_wheel, C_wheel, R, rho, C_d, A_f, C_roll, g, max_steer_deg,
       Vblendmin, Vblendmax;
+  /* workgroup dispatch order of a batch (results do not depend on it: instances are independent):
+     0 = instance order; 1 = (default) the instances whose initial speed is near the ends of the
+     range (<= 16.5 or >= 39 m/s: through the 15 m/s blend corner / the hardest contouring cases, the
+     ones that run hundreds of iterations) first, so the batch's longest solves start early */
+  int32_t dispatch_order;
 } mr_config;
 
 typedef struct mr_inputs {
@@ -115,6 +120,8 @@ typedef struct mr_outputs {
                       steer rows (NaN when state0 has no throttle / steer).  CasADi convention: Lagrangian
                       f + lam_g . g, canonical row = the non-constant side (positive at an active upper
                       bound); unscaled objective.  NULL to skip. */
+  int64_t* timeline; /* optional [2][B] diagnostics: device clock (s_memrealtime, 100 MHz) when instance i's
+                        workgroup started and finished; NULL to skip */
 } mr_outputs;
 
 typedef struct mr_handle mr_handle;

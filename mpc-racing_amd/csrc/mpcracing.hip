@@ -9,6 +9,10 @@
 #include <string>
 
 #include "mr_wave.h"
+// The centerline, sensing and plant kernels are bit-exact against the host build and the oracle
+// (tests/test_gpu_track.py, test_lane_table.py, test_gpu_closed_loop.py): no FMA contraction in the
+// code below (the solver above is built with -ffp-contract=fast, build.py).
+#pragma clang fp contract(off)
 #include "mr_track.h"
 #include "mr_agent.h"
 #include "mr_plant.h"
@@ -18,8 +22,10 @@ using namespace mr;
 
 struct mr_handle {
   mr_config cfg;
+  void* params_dev;  // ProbParams<T> of the handle's precision (device copy, set by upload_params)
   void* ws;
   size_t ws_bytes;
+  int* order;  // [max_batch] workgroup -> instance (mr_order_kernel)
   TyreCoef<double> tf, tr;
   int have_tyres;
 };
@@ -31,6 +37,20 @@ static int fail(int code, const std::string& msg) {
   return code;
 }
 
+// Entry points switch to the handle's device for their HIP calls and restore the caller's current
+// device on return (a library call must not change it).
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
 #define HIP_TRY(x)                                                                  \
   do {                                                                              \
     hipError_t e_ = (x);                                                            \
@@ -39,11 +59,15 @@ static int fail(int code, const std::string& msg) {
 
 // One 64-lane workgroup (= one wavefront) per instance: lanes are stages / matrix rows
 // of that instance (mr_wave.h); the grid is the batch.
-// One wave per SIMD: the full 512-register file for the sweeps (no spills).  The solve is bound by
-// the serial latency of each instance's sweeps, so a second resident wave per SIMD buys little
-// (C4 105.4 vs 104.4 ms, C3 0.418 vs 0.389 s per 8 192-instance batch, 2 vs 1 waves/SIMD).
-#ifndef MR_WAVES_PER_SIMD
-#define MR_WAVES_PER_SIMD 1
+// Waves per SIMD (launch bounds): fp32 2 -- the sweeps fit 256 registers with few spills (the
+// generated dynamics code built without SLP vectorisation, build.py), and a second resident wave
+// hides part of each instance's serial latency (C4 80.3 -> 78.4 ms, profiles/r02_flags_ab.json);
+// fp64 1 -- its sweeps need the full 512-register file (C3 0.418 vs 0.389 s at 2 vs 1 in round 1).
+#ifndef MR_WAVES_PER_SIMD_F32
+#define MR_WAVES_PER_SIMD_F32 2
+#endif
+#ifndef MR_WAVES_PER_SIMD_F64
+#define MR_WAVES_PER_SIMD_F64 1
 #endif
 // Option (MR_SS_LDS=1, fp32 only): the per-stage fields (ss, 38.9 KB) live in LDS, so the
 // sweeps' field loads are LDS round trips instead of Infinity-Cache / HBM ones.  Measured on C4:
@@ -57,28 +81,68 @@ template <typename T>
 struct SSInLDS { static constexpr bool value = MR_SS_LDS && sizeof(T) == 4; };
 
 template <typename T, int MODEL>
-__global__ __launch_bounds__(WL, MR_WAVES_PER_SIMD) void mr_wave_kernel(ProbParams<T> P, mr_inputs in, mr_outputs out, int B, T* ws) {
+__global__ __launch_bounds__(WL, sizeof(T) == 4 ? MR_WAVES_PER_SIMD_F32 : MR_WAVES_PER_SIMD_F64) void mr_wave_kernel(const ProbParams<T>* Pdev, mr_inputs in, mr_outputs out, int B,
+                                                                         T* ws, const int* order) {
   __shared__ T lds[LDS_WORDS];
-  const int i = blockIdx.x;
+  const int i = order ? order[blockIdx.x] : (int)blockIdx.x;
+  const int64_t t_start = out.timeline ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
   Wv w{(int)threadIdx.x};
   MR_GLOBAL T* wsi = (MR_GLOBAL T*)(ws + (int64_t)i * WS_WORDS);
-  // wave-uniform problem and instance constants in LDS: the non-inlined sweeps reach them through
-  // generic references, which would otherwise resolve to the private stack (scratch) copy
-  __shared__ ProbParams<T> Psh;
+  // problem constants: the handle's device copy, read through the constant address space (scalar
+  // loads, SGPRs); instance constants in LDS (every lane writes the same values)
+  const MR_CONST ProbParams<T>& P = *(const MR_CONST ProbParams<T>*)Pdev;
   __shared__ Inst<T> Ish;
-  if (threadIdx.x == 0) Psh = P;
-  __syncthreads();
   // one solver object per lane (its wave-uniform iteration state), also in LDS
   constexpr bool SSL = SSInLDS<T>::value;
   __shared__ alignas(16) char slots[WL * sizeof(WaveSolver<T, MODEL, SSL>)];
   __shared__ T filt_sh[2 * FMAX];  // the line-search filter, shared by the wave
   if constexpr (SSL) {
     __shared__ T ssl[SS_WORDS];
-    solve_instance_wave<T, MODEL, true, true>(Psh, in, out, B, i, wsi, (MR_LDS T*)lds, w, (MR_LDS T*)ssl, &Ish,
+    solve_instance_wave<T, MODEL, true, true>(P, in, out, B, i, wsi, (MR_LDS T*)lds, w, (MR_LDS T*)ssl, &Ish,
                                               slots, (MR_LDS T*)filt_sh);
   } else {
-    solve_instance_wave<T, MODEL, false, true>(Psh, in, out, B, i, wsi, (MR_LDS T*)lds, w, wsi, &Ish, slots,
+    solve_instance_wave<T, MODEL, false, true>(P, in, out, B, i, wsi, (MR_LDS T*)lds, w, wsi, &Ish, slots,
                                                (MR_LDS T*)filt_sh);
+  }
+  if (out.timeline && threadIdx.x == 0) {
+    out.timeline[i] = t_start;
+    out.timeline[(int64_t)B + i] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  }
+}
+
+// Dispatch order (mr_config.dispatch_order = 1): a stable partition of the batch putting first the
+// instances whose initial speed is near the ends of the sampled range -- through the 15 m/s blend
+// corner, or fast enough that the contouring problem is hardest -- which are the ones that run
+// hundreds of iterations (profiles/r02_tail_audit.json).  Workgroups are dispatched roughly in
+// index order, so these long solves start early instead of extending the batch.  One workgroup of
+// 1024 threads: per-thread chunk counts, an LDS scan, then every thread writes its chunk.
+constexpr int kOrderThreads = 1024;
+__global__ __launch_bounds__(kOrderThreads) void mr_order_kernel(const double* state0, int B, int* order) {
+  __shared__ int cnt[kOrderThreads];
+  const int t = threadIdx.x;
+  const int per = (B + kOrderThreads - 1) / kOrderThreads;
+  const int lo = min(B, t * per), hi = min(B, lo + per);
+  auto prio = [&](int i) {
+    const double vx = state0[3 * (int64_t)B + i], vy = state0[4 * (int64_t)B + i];
+    const double v = sqrt(vx * vx + vy * vy);
+    return !(v > 16.5 && v < 39.0);  // NaN speeds go first too
+  };
+  int c = 0;
+  for (int i = lo; i < hi; ++i) c += prio(i) ? 1 : 0;
+  cnt[t] = c;
+  __syncthreads();
+  for (int off = 1; off < kOrderThreads; off <<= 1) {  // inclusive scan (Hillis-Steele)
+    const int v = t >= off ? cnt[t - off] : 0;
+    __syncthreads();
+    cnt[t] += v;
+    __syncthreads();
+  }
+  const int total = cnt[kOrderThreads - 1];
+  int pa = cnt[t] - c;            // priority slots before this chunk
+  int pb = total + (lo - pa);     // the others after all priority ones, stable
+  for (int i = lo; i < hi; ++i) {
+    if (prio(i)) order[pa++] = i;
+    else order[pb++] = i;
   }
 }
 
@@ -86,11 +150,31 @@ static size_t ws_bytes_per_instance(const mr_config& c) {
   return (size_t)WS_WORDS * (c.precision == MR_PREC_FP32 ? sizeof(float) : sizeof(double));
 }
 
+// The handle's problem constants to its device buffer (mr_create, mr_set_tyres): the kernels read them
+// through the constant address space.
+static int upload_params(mr_handle* h) {
+  if (h->cfg.precision == MR_PREC_FP64) {
+    ProbParams<double> P;
+    fill_params<double>(h->cfg, h->tf, h->tr, P);
+    HIP_TRY(hipMemcpy(h->params_dev, &P, sizeof(P), hipMemcpyHostToDevice));
+  } else {
+    ProbParams<float> P;
+    fill_params<float>(h->cfg, h->tf, h->tr, P);
+    HIP_TRY(hipMemcpy(h->params_dev, &P, sizeof(P), hipMemcpyHostToDevice));
+  }
+  return MR_OK;
+}
+
 template <typename T, int MODEL>
 static int launch(mr_handle* h, int B, const mr_inputs* in, mr_outputs* out, hipStream_t st) {
-  ProbParams<T> P;
-  fill_params<T>(h->cfg, h->tf, h->tr, P);
-  hipLaunchKernelGGL((mr_wave_kernel<T, MODEL>), dim3(B), dim3(WL), 0, st, P, *in, *out, B, (T*)h->ws);
+  const int* order = nullptr;
+  if (h->cfg.dispatch_order == 1 && B > 1) {
+    hipLaunchKernelGGL(mr_order_kernel, dim3(1), dim3(kOrderThreads), 0, st, in->state0, B, h->order);
+    HIP_TRY(hipGetLastError());
+    order = h->order;
+  }
+  hipLaunchKernelGGL((mr_wave_kernel<T, MODEL>), dim3(B), dim3(WL), 0, st, (const ProbParams<T>*)h->params_dev, *in,
+                     *out, B, (T*)h->ws, order);
   HIP_TRY(hipGetLastError());
   return MR_OK;
 }
@@ -278,6 +362,7 @@ int mr_version(void) { return 100; }
 int mr_eval_dynamics(mr_handle* h, int32_t n, const double* x, const double* u, const double* nu, double* f,
                      double* J, double* H, void* hip_stream) {
   if (!h || !x || !u || !f || n < 0 || (J && (!H || !nu))) return fail(MR_ERR_ARG, "null argument");
+  DeviceGuard dg_(h->cfg.device);
   ProbParams<double> P;
   fill_params<double>(h->cfg, h->tf, h->tr, P);
   hipStream_t st = (hipStream_t)hip_stream;
@@ -309,17 +394,29 @@ int mr_create(mr_handle** out, const mr_config* cfg) {
   if (cfg->precision != MR_PREC_FP64 && cfg->precision != MR_PREC_FP32) return fail(MR_ERR_ARG, "bad precision");
   if (cfg->max_batch < 1) return fail(MR_ERR_ARG, "max_batch < 1");
   if (!(cfg->Ts > 0)) return fail(MR_ERR_ARG, "Ts must be > 0");
-  HIP_TRY(hipSetDevice(cfg->device));
+  DeviceGuard dg_(cfg->device);
   mr_handle* h = new mr_handle();
   h->cfg = *cfg;
   h->have_tyres = 0;
   memset(&h->tf, 0, sizeof(h->tf));
   memset(&h->tr, 0, sizeof(h->tr));
   h->ws_bytes = ws_bytes_per_instance(*cfg) * (size_t)cfg->max_batch;
+  h->order = nullptr;
   hipError_t e = hipMalloc(&h->ws, h->ws_bytes);
+  if (e == hipSuccess) e = hipMalloc((void**)&h->order, sizeof(int) * (size_t)cfg->max_batch);
+  if (e == hipSuccess) e = hipMalloc(&h->params_dev, sizeof(ProbParams<double>));
   if (e != hipSuccess) {
+    if (h->ws) (void)hipFree(h->ws);
+    if (h->order) (void)hipFree(h->order);
     delete h;
     return fail(MR_ERR_HIP, std::string("workspace hipMalloc: ") + hipGetErrorString(e));
+  }
+  {
+    const int rc = upload_params(h);
+    if (rc != MR_OK) {
+      mr_destroy(h);
+      return rc;
+    }
   }
   *out = h;
   return MR_OK;
@@ -328,6 +425,8 @@ int mr_create(mr_handle** out, const mr_config* cfg) {
 int mr_destroy(mr_handle* h) {
   if (!h) return MR_OK;
   if (h->ws) (void)hipFree(h->ws);
+  if (h->order) (void)hipFree(h->order);
+  if (h->params_dev) (void)hipFree(h->params_dev);
   delete h;
   return MR_OK;
 }
@@ -337,7 +436,8 @@ int mr_set_tyres(mr_handle* h, const double* a_front, double Fz_front, const dou
   h->tf = pacejka_coef(a_front, Fz_front);
   h->tr = pacejka_coef(a_back, Fz_back);
   h->have_tyres = 1;
-  return MR_OK;
+  DeviceGuard dg_(h->cfg.device);
+  return upload_params(h);
 }
 
 int64_t mr_workspace_bytes_per_instance(const mr_handle* h) {
@@ -355,7 +455,7 @@ int mr_solve_batch(mr_handle* h, int32_t B, const mr_inputs* in, mr_outputs* out
   const int m = h->cfg.model;
   if ((m == MR_MODEL_BLENDED_PACEJKA || m == MR_MODEL_DYNAMIC_PACEJKA) && !h->have_tyres)
     return fail(MR_ERR_STATE, "Pacejka model needs mr_set_tyres");
-  HIP_TRY(hipSetDevice(h->cfg.device));
+  DeviceGuard dg_(h->cfg.device);
   hipStream_t st = (hipStream_t)hip_stream;
   if (h->cfg.precision == MR_PREC_FP64) return dispatch_model<double>(h, B, in, out, st);
   return dispatch_model<float>(h, B, in, out, st);
@@ -372,7 +472,7 @@ int mr_track_create(mr_track** out, int32_t device, const double* t, int32_t n_t
   const TrackLayout Lay = track_layout(n_t, n_rows);
   std::vector<double> blob(Lay.total);
   track_tables(t, n_t, cx, cy, n_c, err_left, err_right, n_rows, blob.data());
-  HIP_TRY(hipSetDevice(device));
+  DeviceGuard dg_(device);
   mr_track* tr = new mr_track();
   tr->device = device;
   tr->nt = n_t;
@@ -402,7 +502,7 @@ int mr_track_destroy(mr_track* tr) {
     if (!tr) return fail(MR_ERR_ARG, "null track");                                              \
     if (n < 0) return fail(MR_ERR_ARG, "n < 0");                                                 \
     if (n == 0) return MR_OK;                                                                    \
-    HIP_TRY(hipSetDevice(tr->device));                                                           \
+    DeviceGuard dg_(tr->device);                                                           \
     hipLaunchKernelGGL(kernel, dim3((n + kTrackBlock - 1) / kTrackBlock), dim3(kTrackBlock), 0,  \
                        (hipStream_t)hip_stream, tr->view, n, __VA_ARGS__);                       \
     HIP_TRY(hipGetLastError());                                                                  \
@@ -474,7 +574,7 @@ int mr_track_lane_table(const mr_track* centerline, const mr_track* lane, int32_
   if (centerline->device != lane->device) return fail(MR_ERR_ARG, "centerline and lane on different devices");
   if (n < 0) return fail(MR_ERR_ARG, "n < 0");
   if (n == 0) return MR_OK;
-  HIP_TRY(hipSetDevice(centerline->device));
+  DeviceGuard dg_(centerline->device);
   hipLaunchKernelGGL(mr_lane_table_kernel, dim3((n + kLaneWaves - 1) / kLaneWaves), dim3(64 * kLaneWaves), 0,
                      (hipStream_t)hip_stream, centerline->view, lane->view, (int)n, s, dist, s_lane);
   HIP_TRY(hipGetLastError());

@@ -139,5 +139,6 @@ inline void fill_default_config(mr_config* c) {
   c->T_max = 743.0; c->r_wheel = 0.37; c->C_wheel = 2 * 3.14 * 0.37; c->R = 9.0; c->rho = 1.225;
   c->C_d = 0.23; c->A_f = 2.2; c->C_roll = 0.012; c->g = 9.81; c->max_steer_deg = 70.0;
   c->Vblendmin = 2.0; c->Vblendmax = 15.0;
+  c->dispatch_order = 1;
 }
 }  // namespace mr

@@ -193,6 +193,7 @@ template <typename T>
 MR_HD void ipow(T e, int n, T& v, T& d1, T& d2) {
   // e^n, n e^(n-1), n(n-1) e^(n-2) for integer n >= 1
   T p2 = T(1);
+  #pragma unroll
   for (int i = 0; i < n - 2; ++i) p2 *= e;
   if (n >= 2) {
     d2 = T(n) * T(n - 1) * p2;
@@ -294,12 +295,15 @@ MR_HD T stage_cost(const ProbParams<T>& P, const Inst<T>& I, int k, const T* z, 
   val += I.alpha_c * cv + P.alpha_L * e.eL * e.eL;
   const int id3[3] = {0, 1, 6};
   if (g) {
+    #pragma unroll
     for (int a = 0; a < 3; ++a)
       g[id3[a]] += sc * (I.alpha_c * c1 * e.gC[a] + T(2) * P.alpha_L * e.eL * e.gL[a]);
   }
   if (H) {
     int q = 0;
+    #pragma unroll
     for (int a = 0; a < 3; ++a)
+      #pragma unroll
       for (int b = a; b < 3; ++b, ++q) {
         T hv = I.alpha_c * (c2 * e.gC[a] * e.gC[b] + c1 * e.hC[q]) +
                T(2) * P.alpha_L * (e.gL[a] * e.gL[b] + e.eL * e.hL[q]);
@@ -368,8 +372,10 @@ MR_HD void chol3_solve(const T* L, T* b) {  // solves (L L^T) x = b in place
 // y = A v for the augmented dynamics Jacobian w.r.t. x (11x11); J is the 6x8 vehicle Jacobian
 template <typename T>
 MR_HD void apply_A(const T* J, int k, const T* v, T* y) {
+  #pragma unroll
   for (int i = 0; i < 6; ++i) {
     T acc = T(0);
+    #pragma unroll
     for (int j = 0; j < 6; ++j) acc += J[i * 8 + j] * v[j];
     y[i] = acc;
   }
@@ -382,6 +388,7 @@ MR_HD void apply_A(const T* J, int k, const T* v, T* y) {
 // y = B w (11x3)
 template <typename T>
 MR_HD void apply_B(const T* J, int k, const T* w, T* y) {
+  #pragma unroll
   for (int i = 0; i < 6; ++i) y[i] = J[i * 8 + 6] * w[0] + J[i * 8 + 7] * w[1];
   y[6] = w[2];
   y[7] = w[0];
@@ -392,8 +399,10 @@ MR_HD void apply_B(const T* J, int k, const T* w, T* y) {
 // y = A^T v (11)
 template <typename T>
 MR_HD void apply_At(const T* J, int k, const T* v, T* y) {
+  #pragma unroll
   for (int j = 0; j < 6; ++j) {
     T acc = T(0);
+    #pragma unroll
     for (int i = 0; i < 6; ++i) acc += J[i * 8 + j] * v[i];
     y[j] = acc;
   }
@@ -408,6 +417,7 @@ template <typename T>
 MR_HD void apply_Bt(const T* J, int k, const T* v, T* y) {
   T a0 = v[7], a1 = v[8];
   if (k == 0) { a0 += v[9]; a1 += v[10]; }
+  #pragma unroll
   for (int i = 0; i < 6; ++i) { a0 += J[i * 8 + 6] * v[i]; a1 += J[i * 8 + 7] * v[i]; }
   y[0] = a0; y[1] = a1; y[2] = v[6];
 }
@@ -420,7 +430,13 @@ struct SolveOut {
   double kkt, obj;
 };
 
-constexpr int FMAX = 16;
+#ifndef MR_FMAX
+#define MR_FMAX 16
+#endif
+#ifndef MR_LS_FAIL_MAX
+#define MR_LS_FAIL_MAX 1000000
+#endif
+constexpr int FMAX = MR_FMAX;
 
 template <typename T, int MODEL>
 struct Solver {
@@ -1001,6 +1017,7 @@ struct Solver {
     SolveOut out{2, 0, 0.0, 0.0};
     T mu_prev = mu;
     int acc_count = 0;
+    int ls_fail = 0;  // consecutive iterations without an acceptable line-search step
     int it = 0;
     for (it = 0;; ++it) {
       MR_PROF(0, eval_sweep(mu_prev));
@@ -1062,7 +1079,9 @@ struct Solver {
       T alpha = ap;
       bool accepted = false, ftype = false;
       int nls = 0;
-      while (alpha >= a_min) {
+      // backtracking ends below a_min, or below 1e-30: a_min is 0 when theta is (and may flush to 0
+      // in fp32), and halving alpha to 0 would never leave the loop
+      while (alpha >= a_min && alpha >= T(1e-30)) {
         for (int pass = 0; pass < 2 && !accepted; ++pass) {
           bool soc = pass == 1;
           T th_t, ph_t;
@@ -1087,8 +1106,11 @@ struct Solver {
         alpha *= T(0.5);
         nls++;
       }
+      // no acceptable step: see mr_wave.h (same rule)
+      ls_fail = accepted ? 0 : ls_fail + 1;
+      if (ls_fail >= MR_LS_FAIL_MAX) { out.status = 3; break; }
       if (!accepted) {
-        alpha = mr_max(alpha, a_min);
+        alpha = mr_min(mr_max(alpha, a_min), ap);
         T th_t, ph_t;
         trial(alpha, false, th_t, ph_t);
         ftype = false;

@@ -49,11 +49,17 @@
 #define MR_ASSUME_LDS_STATE()                                      \
   do {                                                             \
     __builtin_assume(__builtin_amdgcn_is_shared((const void*)this));  \
-    __builtin_assume(__builtin_amdgcn_is_shared((const void*)&P));    \
     __builtin_assume(__builtin_amdgcn_is_shared((const void*)&I));    \
   } while (0)
 #else
 #define MR_ASSUME_LDS_STATE() ((void)0)
+#endif
+
+// the wave-uniform view of the problem constants inside a WaveSolver method (shadows the member)
+#define MR_UNIFORM_P() const ProbParams<T>& P = *(const ProbParams<T>*)wu_ptr(&this->P)
+
+#ifndef MR_PHASE_CYCLES
+#define MR_PHASE_CYCLES 0  // 1: per-sweep shader-cycle counters of the trace instance (tools/phase_probe.py)
 #endif
 
 namespace mr {
@@ -61,12 +67,15 @@ namespace mr {
 struct SSF {
   enum {
     Z0 = 0, Z1 = Z0 + NZS, DZ = Z1 + NZS, S0 = DZ + NZS, S1 = S0 + NI, LAM = S1 + NI, DLAM = LAM + NI,
-    DS = DLAM + NI, NU = DS + NI, DNU = NU + NX, NF = DNU + NX
+    DS = DLAM + NI, NU = DS + NI, DNU = NU + NX, GL = DNU + NX, NF = GL + NZ
   };
 };
+// Stage record (stage-major, RC_STRIDE words per stage): the evaluation sweep's stage QP data
+// (Jacobian, defect, Hessian, gradients), then the Riccati sweep's outputs.
 struct RCF {
   enum {
-    H = 0, G0 = H + NH, G1 = G0 + NZ, GL = G1 + NZ, J = GL + NZ, C = J + 48, P = C + NX, PV0 = P + NP,
+    J = 0, C = J + 48, H = C + NX, G0 = H + NH, G1 = G0 + NZ,
+    P = G1 + NZ, PV0 = P + NP,
     PV1 = PV0 + NX, K = PV1 + NX, K0 = K + NU * NX, K1 = K0 + NU, ACL = K1 + NU, FF = ACL + NX * NX,
     CONE = FF + NX, CZERO, SELP, SEL0,  // constants 1, 0, [k > 0], [k == 0] (written once per solve)
     JUNK, NF                           // discard slot of the branch-free stores (any lane)
@@ -165,7 +174,9 @@ constexpr int SS_WORDS = SSF::NF * WL;
 
 template <typename T, int MODEL, bool SSL = false>
 struct WaveSolver {
-  const ProbParams<T>& P;
+  // problem constants: device memory read through a constant-address-space pointer made wave-uniform
+  // in every method (MR_UNIFORM_P), so they are scalar loads into SGPRs, not VGPRs
+  const MR_CONST ProbParams<T>& P;
   const Inst<T>& I;
   Wv w;
   typename SSPtr<T, SSL>::type ss;
@@ -193,9 +204,11 @@ struct WaveSolver {
   T res_ap, res_ad, res_gphi, res_th, res_ph;
   double* trace = nullptr;
   int trace_cap = 0;
+#if MR_PHASE_CYCLES
   unsigned long long tsub[4] = {0, 0, 0, 0};  // diagnostics: sub-phase cycles of the trace instance
+#endif
 
-  MR_HD WaveSolver(const ProbParams<T>& P_, const Inst<T>& I_, Wv w_, MR_GLOBAL T* ws, MR_LDS T* lds_,
+  MR_HD WaveSolver(const MR_CONST ProbParams<T>& P_, const Inst<T>& I_, Wv w_, MR_GLOBAL T* ws, MR_LDS T* lds_,
                    typename SSPtr<T, SSL>::type ss_)
       : P(P_), I(I_), w(w_), ss(ss_), rc(ws + (int64_t)SSF::NF * WL), lds(lds_), N(P_.N), ln(w_.lane) {}
 
@@ -204,6 +217,7 @@ struct WaveSolver {
   MR_HD auto& fph(int i) const { return filt[FMAX + i]; }
   MR_HD MR_GLOBAL T* R(int k) const { return rc + (int64_t)k * RC_STRIDE; }
   MR_HD bool own() const { return ln <= N; }
+
   MR_HD int zf(int b) const { return b ? SSF::Z1 : SSF::Z0; }
   MR_HD int sf(int b) const { return b ? SSF::S1 : SSF::S0; }
   MR_HD int nxt() const { return (ln + 1) & (WL - 1); }
@@ -214,6 +228,7 @@ struct WaveSolver {
   }
 
   MR_HD void row_values(int k, const T* z, const Err<T>& e, T* d, int* act) const {
+    MR_UNIFORM_P();
 #pragma unroll
     for (int r = 0; r < NROW; ++r) {
       int a;
@@ -230,6 +245,7 @@ struct WaveSolver {
   }
 
   MR_HD void lane_block(int b, const T* d, T& htt, T& hd, T& gt0, T& gt1) const {
+    MR_UNIFORM_P();
     htt = T(0); gt0 = sc * P.lane_pen; gt1 = T(0);
     T sig[3];
     for (int q = 0; q < 3; ++q) {
@@ -244,6 +260,7 @@ struct WaveSolver {
 
   // ---------------- initialisation (MPC.py:100-131) ----------------
   MR_SWEEP void init(const double* u_init, int64_t ustride) {
+    MR_UNIFORM_P();
     cur = 0;
     T z[NZS], zn[NX], my[NZS];
     for (int i = 0; i < NZS; ++i) { z[i] = T(0); my[i] = T(0); }
@@ -321,6 +338,7 @@ struct WaveSolver {
   // ---------------- sweep 1: evaluation, KKT error terms, stage QP data (lane = stage) ----------------
   MR_SWEEP void eval_sweep(T mu_prev) {
     MR_ASSUME_LDS_STATE();
+    MR_UNIFORM_P();
     const T kappa_sigma = T(1e10);
     const int k = ln;
     T st_l = T(0), pr_l = T(0), th_l = T(0), smax_l = T(0), smin_l = T(1e30), nu1_l = T(0), lam1_l = T(0),
@@ -344,7 +362,9 @@ struct WaveSolver {
       nun[i] = wshfl(w, nuk[i], nxt());
       znext[i] = wshfl(w, z[i], nxt());
     }
+#if MR_PHASE_CYCLES
     const unsigned long long te0 = trace ? MR_CLOCK() : 0ull;
+#endif
     if (own()) {
       MR_GLOBAL T* Rk = R(k);
       T H[NH], g0[NZ], g1[NZ], gl[NZ], st[NZ];
@@ -379,7 +399,7 @@ struct WaveSolver {
       Err<T> e;
       errors(I, z[0], z[1], z[6], e, true);
       f_l += stage_cost(P, I, k, z, e, sc, gl, H);
-      for (int i = 0; i < NZ; ++i) { g0[i] += gl[i]; st[i] += gl[i]; }
+      for (int i = 0; i < NZ; ++i) { g0[i] += gl[i]; st[i] += gl[i]; S(SSF::GL + i) = gl[i]; }
       if (k >= 1)
         for (int i = 0; i < NX; ++i) st[i] -= nuk[i];
       T d[NI];
@@ -456,9 +476,11 @@ struct WaveSolver {
       if (k < N)
         for (int i = NX; i < NZ; ++i) st_l = mr_max(st_l, mr_abs(st[i]));
       for (int i = 0; i < NH; ++i) Rk[RCF::H + i] = H[i];
-      for (int i = 0; i < NZ; ++i) { Rk[RCF::G0 + i] = g0[i]; Rk[RCF::G1 + i] = g1[i]; Rk[RCF::GL + i] = gl[i]; }
+      for (int i = 0; i < NZ; ++i) { Rk[RCF::G0 + i] = g0[i]; Rk[RCF::G1 + i] = g1[i]; }
     }
+#if MR_PHASE_CYCLES
     const unsigned long long te1 = trace ? MR_CLOCK() : 0ull;
+#endif
     stat_max = wmax(w, st_l);
     pr_max = wmax(w, pr_l);
     theta = wsum(w, th_l);
@@ -471,7 +493,9 @@ struct WaveSolver {
     mi = wsum(w, mi_l);
     me = NX * (N + 1);
     wsync(w);  // stage records visible to every lane before the Riccati sweep
+#if MR_PHASE_CYCLES
     if (trace) { tsub[2] += te1 - te0; tsub[3] += MR_CLOCK() - te1; }
+#endif
   }
 
   MR_HD T kkt_error(T m) const {
@@ -585,7 +609,6 @@ struct WaveSolver {
     const Wv w = this->w;
     MR_GLOBAL T* const rcb = rc;
     MR_LDS T* const LP = lds + LP_OFF;
-    MR_LDS T* const LX = lds + LX_OFF;
     auto R = [rcb](int k) { return rcb + (int64_t)k * RC_STRIDE; };
     for (int q = l; q < 16 * LDS_LD; q += WL) LP[q] = T(0);
     wsync_lds(w);
@@ -630,24 +653,30 @@ struct WaveSolver {
       frag_finish(dd, raw_use, eb, dq, ab, dacl);
       frag_load(R(k >= 1 ? k - 1 : 0), fp, raw_fill);  // unconditional: k = 0 re-reads its own record
       // X = P^ E^  (A fragment s: P^[c][4s+g])
-      T dx[4] = {T(0), T(0), T(0), T(0)};
+      // two independent 2-MFMA accumulation chains (k = 0..7 | 8..15) instead of one 4-long
+      // dependent chain: half the MFMA latency on the stage's critical path
+      T dx[4] = {T(0), T(0), T(0), T(0)}, dx2[4] = {T(0), T(0), T(0), T(0)};
+      wmfma(w, LP[c * LDS_LD + g], eb[0], dx);
+      wmfma(w, LP[c * LDS_LD + 8 + g], eb[2], dx2);
+      wmfma(w, LP[c * LDS_LD + 4 + g], eb[1], dx);
+      wmfma(w, LP[c * LDS_LD + 12 + g], eb[3], dx2);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) wmfma(w, LP[c * LDS_LD + 4 * s + g], eb[s], dx);
+      for (int v = 0; v < 4; ++v) dx[v] += dx2[v];
       // B fragments X[4s+g][c]
       T xb[4];
-      if (sizeof(T) == 8) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) xb[s] = dx[s];  // f64: register s already holds row g + 4s
-      } else {
-#pragma unroll
-        for (int v = 0; v < 4; ++v) LX[(4 * g + v) * LDS_LD + c] = dx[v];
-        wsync_lds(w);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) xb[s] = LX[(4 * s + g) * LDS_LD + c];
-      }
+      for (int s = 0; s < 4; ++s) xb[s] = dx[s];  // f64: register s already holds row g + 4s
+      if constexpr (sizeof(T) == 4) wtranspose4(w, xb);  // f32: D rows 4g+v -> B rows 4s+g, in registers
       // Q = (H + delta I | g0 | g1) + E^T X
+      {
+        T dq2[4] = {T(0), T(0), T(0), T(0)};
+        wmfma(w, eb[0], xb[0], dq);
+        wmfma(w, eb[2], xb[2], dq2);
+        wmfma(w, eb[1], xb[1], dq);
+        wmfma(w, eb[3], xb[3], dq2);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) wmfma(w, eb[s], xb[s], dq);
+        for (int v = 0; v < 4; ++v) dq[v] += dq2[v];
+      }
       auto qat = [&](int a, int b) { return wbcast(w, dq[dreg(a)], dgrp(a) * 16 + b); };
       T Rh[6] = {qat(11, 11), qat(11, 12), qat(11, 13), qat(12, 12), qat(12, 13), qat(13, 13)};
       T L[6], iv[3];
@@ -669,12 +698,12 @@ struct WaveSolver {
       ltsolve3r(L, iv, k1);
       {  // branch-free gain stores (other lanes hit the discard slot): a loop free of divergent
          // branches keeps the waits for the prefetched operands exact across the back-edge
-        const bool kcol = (g == 0) & (c < NX), l0 = l == 0;
+        // row a of K by lanes (0, c < 11), k0[a] by lane (0, 11), k1[a] by lane (0, 12): one store per a
+        const bool kcol = (g == 0) & (c < NX), kf0 = (g == 0) & (c == NX), kf1 = (g == 0) & (c == NX + 1);
 #pragma unroll
         for (int a = 0; a < NU; ++a) {
-          Rk[kcol ? RCF::K + a * NX + c : RCF::JUNK] = -kc[a];
-          Rk[l0 ? RCF::K0 + a : RCF::JUNK] = -k0[a];
-          Rk[l0 ? RCF::K1 + a : RCF::JUNK] = -k1[a];
+          const int idx = kcol ? RCF::K + a * NX + c : (kf0 ? RCF::K0 + a : (kf1 ? RCF::K1 + a : RCF::JUNK));
+          Rk[idx] = kcol ? -kc[a] : (kf0 ? -k0[a] : -k1[a]);
         }
       }
       // closed-loop map (A + B K | B (k0 + mu k1) + c) for the forward recursion
@@ -714,8 +743,11 @@ struct WaveSolver {
   //   i < 11 owns dx[i], the 11 values are shared with v_readlane, one 11-term dot per step.
   //   Then stage-parallel: du_k = K_k dx_k + k0 + mu k1, slack/dual steps, costates.
   MR_SWEEP void forward(T& ap, T& ad, T& gphi) {
+    MR_UNIFORM_P();
     MR_ASSUME_LDS_STATE();
+#if MR_PHASE_CYCLES
     const unsigned long long tf0 = trace ? MR_CLOCK() : 0ull;
+#endif
     const T mu = this->mu;
     const T tau = mr_max(T(0.99), T(1) - mu);
     T dz[NZS];
@@ -726,59 +758,78 @@ struct WaveSolver {
       MR_GLOBAL T* const rcb = rc;
       MR_LDS T* const LDX = lds + LDX_OFF;
       auto R = [rcb](int k) { return rcb + (int64_t)k * RC_STRIDE; };
-      const int i = ln < NX ? ln : 0;
+      // One recursion step per stage k = 0..N with three lane groups sharing the same dot product
+      // row . dx_k (dx_k gathered from lanes 0..10): group 0 (lanes 0..10) row i of the closed-loop
+      // map -> dx_{k+1}[i]; group 1 (lanes 16..26) row i of P_k -> the costate step
+      // dnu_k[i] = P_k dx_k + p_k - nu_k (k >= 1); group 2 (lanes 32..34) row a of K_k ->
+      // du_k[a] = K_k dx_k + k0 + mu k1.  Every lane gathers its row from stage k's record (one
+      // record, a few cache lines per load), instead of each lane reading its own stage's P and K
+      // afterwards (a different cache line per lane and load).  Lanes without a row read the
+      // record's zero slot.
+      const int grp = ln >> 4, r = ln & 15;
+      const bool g0r = (grp == 0) & (r < NX), g1r = (grp == 1) & (r < NX), g2r = (grp == 2) & (r < NU);
+      int roff[NX], c0off, c1off;
+#pragma unroll
+      for (int j = 0; j < NX; ++j)
+        roff[j] = g0r ? RCF::ACL + r * NX + j : (g1r ? RCF::P + pidx(r, j) : (g2r ? RCF::K + r * NX + j : RCF::CZERO));
+      c0off = g0r ? RCF::FF + r : (g1r ? RCF::PV0 + r : (g2r ? RCF::K0 + r : RCF::CZERO));
+      c1off = g1r ? RCF::PV1 + r : (g2r ? RCF::K1 + r : RCF::CZERO);
+      const int rnu = g1r ? r : 0;
+      MR_LDS T* const LDU = lds + LX_OFF;  // du_k[a] at [3 k + a] (the Riccati tiles are dead here)
+      static_assert(3 * WL <= LP_OFF + 16 * LDS_LD, "du staging");
       T dxi = T(0);
       if (ln < NX) LDX[ln] = T(0);
-      // row i of the closed-loop map and f[i], prefetched PD stages ahead (register ring)
 #ifndef MR_FWD_PD
 #define MR_FWD_PD 4
 #endif
-      constexpr int PD = MR_FWD_PD;
-      T ar_r[PD][NX], f_r[PD];
+      constexpr int PD = MR_FWD_PD;  // prefetch distance (stages), register ring
+      T rw_r[PD][NX], c0_r[PD], c1_r[PD], nu_r[PD];
 #pragma unroll
       for (int d = 0; d < PD; ++d) {
-        const int kk = d < N ? d : N - 1;
-        for (int j = 0; j < NX; ++j) ar_r[d][j] = R(kk)[RCF::ACL + i * NX + j];
-        f_r[d] = R(kk)[RCF::FF + i];
+        const int kk = d < N ? d : N;
+        for (int j = 0; j < NX; ++j) rw_r[d][j] = R(kk)[roff[j]];
+        c0_r[d] = R(kk)[c0off];
+        c1_r[d] = R(kk)[c1off];
+        nu_r[d] = ss[(SSF::NU + rnu) * WL + kk];
       }
-      for (int k0 = 0; k0 < N; k0 += PD) {
+      for (int k0 = 0; k0 <= N; k0 += PD) {
 #pragma unroll
         for (int d = 0; d < PD; ++d) {
           const int k = k0 + d;
-          if (k >= N) break;  // wave-uniform
-          T ar[NX];
-          for (int j = 0; j < NX; ++j) ar[j] = ar_r[d][j];
-          const T fi = f_r[d];
-          const int kn = k + PD < N ? k + PD : N - 1;
-          for (int j = 0; j < NX; ++j) ar_r[d][j] = R(kn)[RCF::ACL + i * NX + j];
-          f_r[d] = R(kn)[RCF::FF + i];
+          if (k > N) break;  // wave-uniform
+          T rw[NX];
+          for (int j = 0; j < NX; ++j) rw[j] = rw_r[d][j];
+          const T c0 = c0_r[d], c1 = c1_r[d], nuv = nu_r[d];
+          const int kn = k + PD < N ? k + PD : N;
+          for (int j = 0; j < NX; ++j) rw_r[d][j] = R(kn)[roff[j]];
+          c0_r[d] = R(kn)[c0off];
+          c1_r[d] = R(kn)[c1off];
+          nu_r[d] = ss[(SSF::NU + rnu) * WL + kn];
           T dxv[NX];
           wgather<T, NX>(w, dxi, dxv);
-          T acc = fi;
-          for (int j = 0; j < NX; ++j) acc += ar[j] * dxv[j];
-          dxi = ln < NX ? acc : T(0);
-          if (ln < NX) LDX[(k + 1) * 12 + ln] = dxi;
+          T acc = c0 + mu * c1;
+          for (int j = 0; j < NX; ++j) acc += rw[j] * dxv[j];
+          dxi = g0r ? acc : T(0);
+          if (g0r) LDX[(k + 1) * 12 + r] = dxi;  // row N + 1 <= 64 (N = 63: the discard slots)
+          if (g1r && k >= 1) ss[(SSF::DNU + r) * WL + k] = acc - nuv;
+          if (g2r) LDU[3 * k + r] = acc;
         }
       }
       wsync_lds(w);
       if (ln <= N)
         for (int j = 0; j < NX; ++j) dz[j] = LDX[ln * 12 + j];
-      if (ln < N) {
-        const MR_GLOBAL T* Rk = R(ln);
-        for (int a = 0; a < NU; ++a) {
-          T v = Rk[RCF::K0 + a] + mu * Rk[RCF::K1 + a];
-          for (int j = 0; j < NX; ++j) v += Rk[RCF::K + a * NX + j] * dz[j];
-          dz[NX + a] = v;
-        }
-      }
+      if (ln < N)
+        for (int a = 0; a < NU; ++a) dz[NX + a] = LDU[3 * ln + a];
     }
+#if MR_PHASE_CYCLES
     const unsigned long long tf1 = trace ? MR_CLOCK() : 0ull;
+#endif
     // stage-parallel part
     T ap_l = T(1), ad_l = T(1), g_l = T(0);
     if (own()) {
       const int k = ln;
       MR_GLOBAL T* Rk = R(k);
-      for (int i = 0; i < NZ; ++i) g_l += Rk[RCF::GL + i] * dz[i];
+      for (int i = 0; i < NZ; ++i) g_l += S(SSF::GL + i) * dz[i];
       T z[NZS];
       load_z(cur, z);
       Err<T> e;
@@ -818,22 +869,18 @@ struct WaveSolver {
         if (ds < T(0)) ap_l = mr_min(ap_l, -tau * s / ds);
         if (dl < T(0)) ad_l = mr_min(ad_l, -tau * lam / dl);
       }
-      if (k >= 1) {  // costate step nu_k + dnu_k = P_k dx_k + p_k
-        for (int i = 0; i < NX; ++i) {
-          T v = Rk[RCF::PV0 + i] + mu * Rk[RCF::PV1 + i];
-          for (int l = 0; l < NX; ++l) v += Rk[RCF::P + pidx(i, l)] * dz[l];
-          S(SSF::DNU + i) = v - S(SSF::NU + i);
-        }
-      }
     }
     ap = wmin(w, ap_l);
     ad = wmin(w, ad_l);
     gphi = wsum(w, g_l);
+#if MR_PHASE_CYCLES
     if (trace) { tsub[0] += tf1 - tf0; tsub[1] += MR_CLOCK() - tf1; }
+#endif
   }
 
   // ---------------- sweep 4: line-search trial point (writes buffer 1-cur) ----------------
   MR_SWEEP bool trial(T alpha, bool soc, T& th_t, T& ph_t) {
+    MR_UNIFORM_P();
     MR_ASSUME_LDS_STATE();
     const int nb = 1 - cur;
     const int k = ln;
@@ -923,6 +970,7 @@ struct WaveSolver {
   }
 
   MR_HD T lane_violation() const {
+    MR_UNIFORM_P();
     T v = T(0);
     if (P.lane && own() && ln >= 1) v = S(zf(cur) + 14);
     return wmax(w, v);
@@ -930,17 +978,27 @@ struct WaveSolver {
 
   // ---------------- the IPM loop (wave-uniform control) ----------------
   MR_HD SolveOut solve() {
+    MR_UNIFORM_P();
     const T kappa_eps = T(10), kappa_mu = T(0.2), theta_mu = T(1.5);
     const T mu_min = P.tol / T(10);
     const T s_phi = T(2.3), s_theta = T(1.1), delta_sw = T(1), eta = T(1e-4), g_th = T(1e-5), g_ph = T(1e-5);
     SolveOut out{2, 0, 0.0, 0.0};
     T mu_prev = mu;
     int acc_count = 0;
+    int ls_fail = 0;  // consecutive iterations without an acceptable line-search step
     int it = 0;
-    // diagnostics of the trace instance: shader cycles per phase and call counts
+    // diagnostics of the trace instance: shader cycles per phase and call counts (MR_PHASE_CYCLES
+    // builds only -- the counters stay live across every sweep call, so the product build has none)
+#if MR_PHASE_CYCLES
     unsigned long long cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t0 = 0, tstart = trace ? MR_CLOCK() : 0ull;
 #define MR_T0() (t0 = trace ? MR_CLOCK() : 0ull)
 #define MR_T1(slot) (cyc[slot] += trace ? MR_CLOCK() - t0 : 0ull)
+#define MR_CNT(slot) (cyc[slot]++)
+#else
+#define MR_T0() ((void)0)
+#define MR_T1(slot) ((void)0)
+#define MR_CNT(slot) ((void)0)
+#endif
     for (it = 0;; ++it) {
       MR_T0();
       eval_sweep(mu_prev);
@@ -965,7 +1023,7 @@ struct WaveSolver {
       bool first = true, fact_ok = false;
       MR_T0();
       for (int tries = 0; tries < 60; ++tries) {
-        cyc[6]++;
+        MR_CNT(6);
         if (riccati(delta, mu)) { fact_ok = true; break; }
         if (first) {
           delta = delta_last == T(0) ? T(1e-4) : mr_max(T(1e-20), delta_last / T(3));
@@ -995,15 +1053,17 @@ struct WaveSolver {
       T alpha = ap;
       bool accepted = false, ftype = false;
       int nls = 0;
-      while (alpha >= a_min) {
+      // backtracking ends below a_min, or below 1e-30: a_min is 0 when theta is (and may flush to 0
+      // in fp32), and halving alpha to 0 would never leave the loop
+      while (alpha >= a_min && alpha >= T(1e-30)) {
         for (int pass = 0; pass < 2 && !accepted; ++pass) {
           bool soc = pass == 1;
           T &th_t = res_th, &ph_t = res_ph;
           MR_T0();
           bool ok = trial(alpha, soc, th_t, ph_t);
           MR_T1(3);
-          cyc[4]++;
-          if (soc) cyc[5]++;
+          MR_CNT(4);
+          if (soc) MR_CNT(5);
           if (ok) ok = th_t <= theta_max && filter_ok(th_t, ph_t);
           if (ok) {
             bool sw = gphi < T(0) && alpha * mr_exp(s_phi * mr_log(-gphi)) > delta_sw * th_pow;
@@ -1022,8 +1082,14 @@ struct WaveSolver {
         alpha *= T(0.5);
         nls++;
       }
+      // No acceptable step: IPOPT would enter its feasibility restoration phase; this solver has
+      // none.  It takes the shortest tried step (never past the fraction-to-boundary step, so the
+      // slacks stay positive) and, after MR_LS_FAIL_MAX consecutive failures, stops with status
+      // failed -- IPOPT's "restoration failed" outcome -- instead of spinning to max_iter.
+      ls_fail = accepted ? 0 : ls_fail + 1;
+      if (ls_fail >= MR_LS_FAIL_MAX) { out.status = 3; break; }
       if (!accepted) {
-        alpha = mr_max(alpha, a_min);
+        alpha = mr_min(mr_max(alpha, a_min), ap);
         T &th_t = res_th, &ph_t = res_ph;
         trial(alpha, false, th_t, ph_t);
         ftype = false;
@@ -1043,6 +1109,8 @@ struct WaveSolver {
     out.iters = it;
 #undef MR_T0
 #undef MR_T1
+#undef MR_CNT
+#if MR_PHASE_CYCLES
     if (trace && ln == 0 && trace_cap >= 2) {  // last row: cycles eval, riccati, forward, trial, #trials, #soc, #factorisations, total
       double* tr = trace + 8 * (trace_cap - 1);
       for (int q = 0; q < 7; ++q) tr[q] = (double)cyc[q];
@@ -1050,6 +1118,7 @@ struct WaveSolver {
       double* tr2 = trace + 8 * (trace_cap - 2);  // sub-phases: forward seq/par, eval stage/reduce
       for (int q = 0; q < 4; ++q) tr2[q] = (double)tsub[q];
     }
+#endif
     if (trace && ln == 0 && it < trace_cap - 2) {
       double* tr = trace + 8 * it;
       tr[0] = (double)out.kkt; tr[1] = (double)fval; tr[2] = (double)theta; tr[3] = (double)stat_max;
@@ -1068,7 +1137,7 @@ MR_HD void run_instance(Solver& S, const mr_inputs& in, const mr_outputs& out, i
                         double X0, double Y0, double s0, Wv w);
 
 template <typename T, int MODEL, bool SSL = false, bool OBJ_LDS = false>
-MR_HD void solve_instance_wave(const ProbParams<T>& P, const mr_inputs& in, const mr_outputs& out, int64_t B,
+MR_HD void solve_instance_wave(const MR_CONST ProbParams<T>& P, const mr_inputs& in, const mr_outputs& out, int64_t B,
                                int64_t i, MR_GLOBAL T* ws, MR_LDS T* lds, Wv w,
                                typename SSPtr<T, SSL>::type ssp = nullptr, Inst<T>* Ish = nullptr,
                                void* solver_slots = nullptr, MR_LDS T* filt_sh = nullptr) {
@@ -1173,7 +1242,7 @@ template <typename Solver>
 MR_HD void run_instance(Solver& S, const mr_inputs& in, const mr_outputs& out, int64_t B, int64_t i, int N,
                         double X0, double Y0, double s0, Wv w) {
   typedef decltype(S.mu) T;
-  const ProbParams<T>& P = S.P;
+  const MR_CONST ProbParams<T>& P = S.P;
   const Inst<T>& I = S.I;
   if (out.trace && out.trace_instance == i) { S.trace = out.trace; S.trace_cap = out.trace_cap; }
   S.init(in.u_init ? in.u_init + i : nullptr, B);

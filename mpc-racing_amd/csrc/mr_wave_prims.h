@@ -26,9 +26,11 @@
 #if MR_DEVICE_BUILD
 #define MR_GLOBAL __attribute__((address_space(1)))
 #define MR_LDS __attribute__((address_space(3)))
+#define MR_CONST __attribute__((address_space(4)))
 #else
 #define MR_GLOBAL
 #define MR_LDS
+#define MR_CONST
 #endif
 
 namespace mr {
@@ -100,6 +102,25 @@ __device__ __forceinline__ double wu(const Wv&, double v) {
   const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffLL));
   const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
   return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+// A pointer every lane holds identically, made visibly uniform (SGPR pair): loads through a
+// constant-address-space pointer then become scalar loads (s_load into SGPRs) instead of per-lane
+// vector loads into VGPRs -- the problem constants cost no vector registers.
+template <typename T>
+__device__ __forceinline__ const MR_CONST T* wu_ptr(const MR_CONST T* p) {
+  const unsigned long long v = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return (const MR_CONST T*)(((unsigned long long)hi << 32) | lo);
+}
+
+// the same for a global-memory base pointer (workspace of the instance): addresses become an SGPR
+// base plus a 32-bit lane offset instead of per-lane 64-bit address arithmetic
+template <typename T>
+__device__ __forceinline__ MR_GLOBAL T* wu_gptr(MR_GLOBAL T* p) {
+  const unsigned long long v = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return (MR_GLOBAL T*)(((unsigned long long)hi << 32) | lo);
 }
 
 // out[i] = value of lane i, i < n (compile-time n): one v_readlane per element
@@ -185,6 +206,23 @@ __device__ __forceinline__ T wmax(const Wv& w, T v) {
 template <typename T>
 __device__ __forceinline__ T wmin(const Wv& w, T v) {
   return wreduce(w, v, [](T a, T b) { return b < a ? b : a; });
+}
+
+// 4x4 transpose across the four 16-lane rows of the wave, per column c = lane & 15: on entry lane
+// (g, c) holds d[v] = M[g][v]; on exit d[s] = M[s][g].  This turns an f32 16x16x4 MFMA result
+// (D layout: lane (g, c) register v = row 4g+v) into the next MFMA's B operand (register s = row
+// 4s+g) without an LDS round trip: two v_permlane32_swap (rows {0,1} <-> {2,3}) and two
+// v_permlane16_swap (rows 0 <-> 1, 2 <-> 3).
+__device__ __forceinline__ void wtranspose4(const Wv&, float* d) {
+  unsigned b0 = __float_as_uint(d[0]), b1 = __float_as_uint(d[1]), b2 = __float_as_uint(d[2]),
+           b3 = __float_as_uint(d[3]);
+  auto p02 = __builtin_amdgcn_permlane32_swap(b0, b2, false, false);
+  auto p13 = __builtin_amdgcn_permlane32_swap(b1, b3, false, false);
+  b0 = p02[0]; b2 = p02[1]; b1 = p13[0]; b3 = p13[1];
+  auto p01 = __builtin_amdgcn_permlane16_swap(b0, b1, false, false);
+  auto p23 = __builtin_amdgcn_permlane16_swap(b2, b3, false, false);
+  d[0] = __uint_as_float(p01[0]); d[1] = __uint_as_float(p01[1]);
+  d[2] = __uint_as_float(p23[0]); d[3] = __uint_as_float(p23[1]);
 }
 
 #else  // host fiber emulation -------------------------------------------------------------
@@ -334,6 +372,24 @@ inline void host_wave_run(HostWave& hw, void (*body)(HostWave*, int, void*), voi
   }
   free(hw.stacks);
   hw.stacks = nullptr;
+}
+
+template <typename T>
+inline const T* wu_ptr(const T* p) { return p; }
+template <typename T>
+inline T* wu_gptr(T* p) { return p; }
+
+// host emulation of wtranspose4 (same result: lane (g, c) gets register g of lane (s, c))
+template <typename T>
+inline void wtranspose4(const Wv& w, T* d) {
+  const int g = w.lane >> 4, c = w.lane & 15;
+  T out[4];
+  for (int s = 0; s < 4; ++s) {
+    T t[4];
+    for (int r = 0; r < 4; ++r) t[r] = wshfl(w, d[r], s * 16 + c);
+    out[s] = t[g];
+  }
+  for (int s = 0; s < 4; ++s) d[s] = out[s];
 }
 
 #endif

@@ -26,7 +26,7 @@ class MRConfig(ctypes.Structure):
                                   "min_throttle_delta", "q_v_max", "v_max", "min_s_delta",
                                   "m", "Iz", "lf", "lr", "Cf", "Cr", "T_max", "r_wheel", "C_wheel", "R",
                                   "rho", "C_d", "A_f", "C_roll", "g", "max_steer_deg", "Vblendmin",
-                                  "Vblendmax")]
+                                  "Vblendmax")] + [("dispatch_order", _I32)]
 
 
 class MRInputs(ctypes.Structure):
@@ -36,7 +36,7 @@ class MRInputs(ctypes.Structure):
 class MROutputs(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in ("X", "U", "S", "eC", "eL", "status", "iters", "obj", "kkt",
                                                "trace")] + [("trace_instance", _I32), ("trace_cap", _I32),
-                                                           ("lam_g", ctypes.c_void_p)]
+                                                           ("lam_g", ctypes.c_void_p), ("timeline", ctypes.c_void_p)]
 
 
 # every symbol declared in include/mpcracing.h (checked by tests/test_abi.py)

@@ -107,7 +107,8 @@ class BatchSolver:
         tr = out.get("trace")
         o = abi.MROutputs(*[ptr(out.get(k)) for k in ("X", "U", "S", "eC", "eL", "status", "iters", "obj", "kkt",
                                                       "trace")], int(trace_instance),
-                          int(tr.shape[0]) if tr is not None else 0, ptr(out.get("lam_g")))
+                          int(tr.shape[0]) if tr is not None else 0, ptr(out.get("lam_g")),
+                          ptr(out.get("timeline")))
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
         self._check(self.lib.mr_solve_batch(self.h, B, ctypes.byref(inp), ctypes.byref(o),
                                             ctypes.c_void_p(st.cuda_stream)))

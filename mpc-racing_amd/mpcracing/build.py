@@ -20,6 +20,9 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+DEFAULT_FLAGS = ["-ffp-contract=fast-honor-pragmas", "-fgpu-flush-denormals-to-zero", "-fno-slp-vectorize"]
+
+
 def build_hip(force=False, verbose=True, out=None, flags=None):
     """Build libmpcracing.so (or a developer A/B variant at ``out`` with ``flags`` replacing the
     default code-generation flags; load it with MR_PRODUCT_LIB)."""
@@ -31,11 +34,19 @@ def build_hip(force=False, verbose=True, out=None, flags=None):
     # contraction came from the old lane-per-instance kernel (deleted); the wave kernel with contraction
     # passes every fp64 parity test against the oracle and the GPU-vs-host-build status tests, and is
     # 2.7 % faster on C4 (profiles/r02_fma_ab.json).  The host twin stays -ffp-contract=off (IEEE
-    # reference for the CPU tests).
+    # reference for the CPU tests).  "fast-honor-pragmas" (not "fast", which fuses in the backend
+    # regardless of source pragmas): the centerline / sensing / plant kernels below the
+    # `#pragma clang fp contract(off)` in mpcracing.hip stay bit-exact with the host build.
     # fp32 kernels use the hardware reciprocal / square root / transcendentals (v_rcp, v_sqrt, v_sin,
     # v_exp, v_log: a few ulp) instead of the correctly rounded library sequences -- the fp32 solve is
-    # instruction-latency bound and its KKT noise floor (~1e-3) is far above these errors; fp64 stays IEEE
-    cg = flags if flags is not None else ["-ffp-contract=fast"]
+    # instruction-latency bound and its KKT noise floor (~1e-3) is far above these errors; fp64 stays IEEE.
+    # fp32 denormals flush to zero (-fgpu-flush-denormals-to-zero): every fp32 division / log otherwise
+    # carries a frexp/ldexp range-scaling sequence (~4 extra VALU ops each); no fp32 quantity of the
+    # solve lives near 1e-38.  fp64 (the centerline kernels, fp64 solves) keeps IEEE denormals.
+    # No SLP vectorisation (-fno-slp-vectorize): the v_pk_* pairs it formed in the generated dynamics
+    # code cost more register moves than they saved (eval sweep 4 975 -> 3 939 VALU instructions, its
+    # scratch spills gone).  A/B on C4: profiles/r02_flags_ab.json.
+    cg = flags if flags is not None else DEFAULT_FLAGS
     cmd = [HIPCC, "--offload-arch=gfx950", "-O3", *cg, "-std=c++17", "-fPIC", "-shared",
            "-Wno-unused-result", "-fno-hip-fp32-correctly-rounded-divide-sqrt", "-fgpu-approx-transcendentals",
            "-o", out, os.path.join(CSRC, "mpcracing.hip")]

@@ -1,5 +1,11 @@
 """Developer probe: per-phase shader cycles of single instances (trace instance, last
-trace row) and B=1 wall latency; writes gpurun_out/phase_probe.json."""
+trace row) and B=1 wall latency; writes gpurun_out/phase_probe.json.
+
+Needs a diagnostic build with the cycle counters compiled in (the product build has none):
+  python -c "import sys; sys.path.insert(0,'mpc-racing_amd'); from mpcracing import build; \
+             build.build_hip(force=True, out='variants/lib_cycles.so', \
+             flags=build.DEFAULT_FLAGS + ['-DMR_PHASE_CYCLES=1'])"
+  MR_PRODUCT_LIB=variants/lib_cycles.so python mpc-racing_amd/tools/phase_probe.py C4"""
 import json
 import os
 import sys

@@ -11,8 +11,12 @@ FETCH_SIZE (KiB) reports half of the bytes of wide coalesced reads on gfx950 -> 
 latency probe) are averaged.
 """
 import csv
+import hashlib
 import json
+import os
 import sys
+
+LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "csrc", "libmpcracing.so")
 
 
 def rows(path):
@@ -52,6 +56,8 @@ def main():
     if f is not None and w is not None:
         res["hbm_bytes_per_launch"] = (2.0 * f + w) * 1024.0
     res["dispatches"] = [nf, nw]
+    with open(os.environ.get("MR_PRODUCT_LIB") or LIB, "rb") as f:  # bench.py reports traffic only for this build
+        res["lib_sha"] = hashlib.sha256(f.read()).hexdigest()[:16]
     if len(sys.argv) > 6:
         res["B"] = int(sys.argv[6])
     if len(sys.argv) > 7:

@@ -581,7 +581,7 @@ def solve_ipm(prob, tol=1e-10, max_iter=300, w0=None, verbose=False, soc=True):
         f_type = False
         w_new = s_new = None
         nls = 0
-        while alpha >= a_min:
+        while alpha >= a_min and alpha >= 1e-30:  # same floor as mr_solver.h / mr_wave.h
             cands = [(w + alpha * dz, s + alpha * ds)]
             if nls == 0 and soc:
                 pass

@@ -60,7 +60,7 @@ def solve(cfg, batch, tyres=None, nthreads=8, trace_instance=-1, trace_cap=0, sc
     if duals:
         out["lam_g"] = np.zeros((13 * N + 9, B))
     o = abi.MROutputs(*[_p(out.get(k)) for k in ("X", "U", "S", "eC", "eL", "status", "iters", "obj", "kkt",
-                                                 "trace")], trace_instance, trace_cap, _p(out.get("lam_g")))
+                                                 "trace")], trace_instance, trace_cap, _p(out.get("lam_g")), None)
     if tyres is not None:
         (af, Fzf), (ar, Fzr) = tyres
         af = np.asarray(af, np.float64)

