@@ -61,6 +61,9 @@
 #ifndef MR_PHASE_CYCLES
 #define MR_PHASE_CYCLES 0  // 1: per-sweep shader-cycle counters of the trace instance (tools/phase_probe.py)
 #endif
+#ifndef MR_PRIO_ITER
+#define MR_PRIO_ITER 0  // > 0: the wave raises its issue priority (s_setprio) at this iteration
+#endif
 
 namespace mr {
 
@@ -1000,6 +1003,11 @@ struct WaveSolver {
 #define MR_CNT(slot) ((void)0)
 #endif
     for (it = 0;; ++it) {
+#if MR_DEVICE_BUILD && MR_PRIO_ITER > 0
+      // long solves: raise the wave's issue priority over the partner wave on its SIMD, so the
+      // batch's slowest instances (which set its makespan) are not slowed by the short ones
+      if (it == MR_PRIO_ITER) __builtin_amdgcn_s_setprio(3);
+#endif
       MR_T0();
       eval_sweep(mu_prev);
       MR_T1(0);

@@ -23,6 +23,9 @@ if [ "$what" = all ] || [ "$what" = bench ]; then
   step bench 900 python bench.py
   step prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-latency
 fi
+if [ "$what" = all ] || [ "$what" = bench ] || [ "$what" = timeline ]; then
+  step timeline 300 python -u mpc-racing_amd/tools/timeline_probe.py C4 1
+fi
 if [ "$what" = probe ]; then
   step fp32_probe 600 python -u mpc-racing_amd/tools/fp32_probe.py 256 4
 fi

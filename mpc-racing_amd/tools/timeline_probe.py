@@ -50,7 +50,7 @@ def main():
         torch.cuda.synchronize()
         t = o1["timeline"].cpu().numpy()[:, 0].astype(np.float64) / 1e5
         solo.append(float(t[1] - t[0]))
-    slots = 1024  # 256 CUs x 4 SIMDs, one wave each
+    slots = 1024 * (2 if wl.CONFIGS[name]["precision"] == "fp32" else 1)  # 256 CUs x 4 SIMDs x waves/SIMD
     rec = {"config": name, "dispatch_order": order, "B": int(B), "makespan_ms": mk,
            "sum_instance_ms": float(dur.sum()), "slot_utilisation": float(dur.sum() / (slots * mk)),
            "ms_per_iter_batch_median": float(np.median(dur / np.maximum(it, 1))),

@@ -24,6 +24,8 @@ def run(cl, state0, ticks, N=15, model="blend", start_control_at=2, dt=0.05, Ts=
     old_yaw = [None] * B
     cmd_thr, cmd_brake, cmd_steer = np.zeros(B), np.zeros(B), np.zeros(B)
     last_controls = None
+    rt = np.asarray(runtime, dtype=np.float64)  # shared (5,) or per vehicle [5][B] (a GA population)
+    rt = np.tile(rt.reshape(5, 1), (1, B)) if rt.size == 5 else rt.reshape(5, B).copy()
     cfg = solver_cfg if solver_cfg is not None else ht.config(N, "dyn", "fp64", False, Ts)
     recs = []
     for step in range(ticks):
@@ -46,7 +48,7 @@ def run(cl, state0, ticks, N=15, model="blend", start_control_at=2, dt=0.05, Ts=
             batch = dict(state0=np.stack([X, Y, yaw, vx, vy, yawdot, thr0, cmd_steer]), s0=prog,
                          cx=np.array([r[2] for r in sense]).T, cy=np.array([r[3] for r in sense]).T,
                          max_error=np.array([r[4] for r in sense]),
-                         runtime=np.tile(np.array(runtime, dtype=np.float64).reshape(5, 1), (1, B)),
+                         runtime=rt,
                          u_init=None if last_controls is None else
                          np.concatenate([last_controls[:, 1:], last_controls[:, -1:]], axis=1))
             out = ht.solve(cfg, batch)

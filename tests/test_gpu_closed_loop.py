@@ -112,3 +112,40 @@ def test_closed_loop_matches_cpu_loop(dtrack):
     # the cars are driving along the track under MPC control
     assert (recs[-1]["progress"].cpu().numpy() > recs[0]["progress"].cpu().numpy()).all()
     assert (np.abs(recs[-1]["error"].cpu().numpy()) < 2.0).all()
+
+
+def test_ga_evaluate_population_matches_cpu_loop(dtrack):
+    """GA fitness (GA/mpcGA.py:16-62): population x segments vehicles of one batched
+    closed loop on the GPU vs the CPU loop (oracle sensing and plant, host build of the solver) driving the
+    same vehicles with the same per-individual RuntimeControllerParameters; segment times and rewards."""
+    import closed_loop_ref
+    import host_twin as ht
+    from mpcracing import ga
+    from mpcracing.closed_loop import ClosedLoop
+    N, ticks, v0 = 15, 40, 14.0
+    pop = np.array([[1000.0, 0.85, 50.0, 2.0, 5000.0],     # RuntimeControllerParameters defaults
+                    [600.0, 0.85, 20.0, 3.0, 2000.0]])
+    bounds = np.array([120.0, 135.0, 150.0])              # two 15 m segments
+    times, recs = ga.evaluate_population(dtrack, pop, bounds, ticks, v0=v0, N=N, tol=1e-10, acceptable_iter=0)
+    P, K = pop.shape[0], len(bounds) - 1
+    s0 = np.tile(bounds[:-1], P)
+    x0 = ClosedLoop.start_states(dtrack, s0, v0=v0)
+    rt = np.repeat(pop, K, axis=0).T.copy()
+    rt[1] = 0.85  # the NLP reads the class-attribute d_max (MPC.py:50)
+    cfg = ht.config(N, "dyn", "fp64", False, 0.05, tol=1e-10, acceptable_iter=0)
+    ref, _ = closed_loop_ref.run(_oracle_cl(), x0, ticks, N=N, model="blend", start_control_at=1,
+                                 runtime=rt, solver_cfg=cfg)
+    for r, c in zip(recs, ref):
+        if r["controlled"]:
+            assert np.array_equal(r["status"].cpu().numpy(), c["status"])
+        np.testing.assert_allclose(r["progress"].cpu().numpy(), c["progress"], rtol=1e-6, atol=1e-6)
+    ref_prog = [{"progress": torch.from_numpy(c["progress"])} for c in ref]
+    tref = ga.segment_times(ref_prog, s0, np.tile(bounds[1:], P), dtrack.length, 0.05).reshape(P, K)
+    assert np.isfinite(times[0]).all(), times  # the default parameters cover both segments
+    np.testing.assert_allclose(times, tref, rtol=1e-6, atol=1e-6)  # inf (segment not reached) where the CPU's is
+    # the individuals differ in the controller, so they differ in segment time
+    assert (times[0] != times[1]).any()
+    r, avg = ga.rewards(times, [1.0] * K)
+    rr, aref = ga.rewards(tref, [1.0] * K)
+    np.testing.assert_allclose(r, rr, rtol=1e-6)
+    np.testing.assert_allclose(avg, aref, rtol=1e-6)
