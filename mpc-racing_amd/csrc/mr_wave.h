@@ -61,6 +61,9 @@
 #ifndef MR_PHASE_CYCLES
 #define MR_PHASE_CYCLES 0  // 1: per-sweep shader-cycle counters of the trace instance (tools/phase_probe.py)
 #endif
+#ifndef MR_FWD_TREE
+#define MR_FWD_TREE 0  // 1: the forward recursion's dot products as three chains (A/B option)
+#endif
 #ifndef MR_PRIO_ITER
 #define MR_PRIO_ITER 0  // > 0: the wave raises its issue priority (s_setprio) at this iteration
 #endif
@@ -208,7 +211,7 @@ struct WaveSolver {
   double* trace = nullptr;
   int trace_cap = 0;
 #if MR_PHASE_CYCLES
-  unsigned long long tsub[4] = {0, 0, 0, 0};  // diagnostics: sub-phase cycles of the trace instance
+  unsigned long long tsub[6] = {0, 0, 0, 0, 0, 0};  // diagnostics: sub-phase cycles of the trace instance
 #endif
 
   MR_HD WaveSolver(const MR_CONST ProbParams<T>& P_, const Inst<T>& I_, Wv w_, MR_GLOBAL T* ws, MR_LDS T* lds_,
@@ -581,9 +584,9 @@ struct WaveSolver {
       fp.lp2[v] = up ? c * LDS_LD + a : fp.lp1[v];
     }
   }
-  static MR_HD void frag_load(const MR_GLOBAL T* Rk, const FragPlan& fp, T* raw) {
+  static MR_HD void frag_load(const WBuf<T>& rb, unsigned ro, const FragPlan& fp, T* raw) {
 #pragma unroll
-    for (int q = 0; q < 13; ++q) raw[q] = Rk[fp.off[q]];
+    for (int q = 0; q < 13; ++q) raw[q] = rb.ld(ro, (unsigned)fp.off[q]);
   }
   // operands straight from the gathered words (constants come from the record's constant slots)
   static MR_HD void frag_finish(const T* dd, const T* raw, T* eb, T* hc, T& ab, T* ac) {
@@ -605,14 +608,16 @@ struct WaveSolver {
   //   P^   = Q_x. - W^T W                 1 x v_mfma          (upper triangle mirrored)
   //   K = -L^{-T} W_x,  k0 | k1 = -L^{-T} w0 | w1, and the closed-loop map for the forward pass
   //   A + B K | B (k0 + mu k1) + c        1 x v_mfma
-  // Stage k-1's record is gathered (13 loads per lane) while stage k is factorised.
+  // Stage k-2's record is gathered (13 loads per lane) while stage k is factorised.
   MR_SWEEP bool riccati(T delta, T mu) {
     MR_ASSUME_LDS_STATE();
     const int l = ln, N = wu(w, this->N), g = l >> 4, c = l & 15;
     const Wv w = this->w;
-    MR_GLOBAL T* const rcb = rc;
+    // the instance's records as a wave-uniform buffer: gathers and stores are (uniform stage offset,
+    // 32-bit lane offset) buffer operations
+    const WBuf<T> rb(rc, (unsigned)WL * (unsigned)RC_STRIDE);
     MR_LDS T* const LP = lds + LP_OFF;
-    auto R = [rcb](int k) { return rcb + (int64_t)k * RC_STRIDE; };
+    auto R = [](int k) { return (unsigned)k * (unsigned)RC_STRIDE; };  // word offset of stage k's record
     for (int q = l; q < 16 * LDS_LD; q += WL) LP[q] = T(0);
     wsync_lds(w);
     FragPlan fp;
@@ -624,37 +629,42 @@ struct WaveSolver {
     // step has no lane-divergent branches
     const T sg[3] = {g == 0 ? T(1) : T(0), g == 1 ? T(1) : T(0), g == 2 ? T(1) : T(0)};
     const T sk = ((g < NU) & (c < NX)) ? T(-1) : T(0), sf = ((g < NU) & (c == 14)) ? T(-1) : T(0);
-    T raw_a[13], raw_b[13];
-    frag_load(R(N - 1), fp, raw_a);
+    // operand gathers run two stages ahead of the factorisation (three rotating buffers): a record
+    // gather is an Infinity-Cache / HBM round trip (the 8 192 instances' records do not fit the L2),
+    // longer than one stage's arithmetic
+    T raw_a[13], raw_b[13], raw_c[13];
+    frag_load(rb, R(N - 1), fp, raw_a);
+    frag_load(rb, R(N >= 2 ? N - 2 : 0), fp, raw_b);
     {  // terminal cost-to-go: P_N = H_N,xx + delta I, p_N = g_N.  Branch-free (lanes >= NX write
        // discard slots), so at least as many memory ops follow the first prefetch on this path as
        // on the loop back-edge and the wait at the loop head stays exact.
-      MR_GLOBAL T* Rn = R(N);
+      const unsigned Rn = R(N);
       const bool row = l < NX;
       const int lr = row ? l : 0, jl = RCF::JUNK, jd = LJUNK_OFF - LP_OFF + l;
       T hv[NX];  // all loads ahead of the stores (the compiler cannot disambiguate H from P)
 #pragma unroll
-      for (int j = 0; j < NX; ++j) hv[j] = Rn[RCF::H + hidx(lr, j)];
-      const T p0 = Rn[RCF::G0 + lr], p1 = Rn[RCF::G1 + lr];
+      for (int j = 0; j < NX; ++j) hv[j] = rb.ld(Rn, RCF::H + hidx(lr, j));
+      const T p0 = rb.ld(Rn, RCF::G0 + lr), p1 = rb.ld(Rn, RCF::G1 + lr);
 #pragma unroll
       for (int j = 0; j < NX; ++j) {
         const T v = hv[j] + (l == j ? delta : T(0));
         LP[row ? l * LDS_LD + j : jd] = v;
-        Rn[(row && j >= l) ? RCF::P + pidx(lr, j) : jl] = v;
+        rb.st(v, Rn, (row && j >= l) ? RCF::P + pidx(lr, j) : jl);
       }
       LP[row ? l * LDS_LD + 11 : jd] = p0;
       LP[row ? l * LDS_LD + 12 : jd] = p1;
-      Rn[row ? RCF::PV0 + l : jl] = p0;
-      Rn[row ? RCF::PV1 + l : jl] = p1;
+      rb.st(p0, Rn, row ? RCF::PV0 + l : jl);
+      rb.st(p1, Rn, row ? RCF::PV1 + l : jl);
     }
     wsync_lds(w);
-    // one stage; the loop below is unrolled by two so the prefetch buffers alternate roles
+    // one stage; the loop below is unrolled by three so the prefetch buffers rotate roles
     // (no register copies of in-flight loads, hence exact vmcnt waits instead of vmcnt(0))
     auto step = [&](int k, const T* raw_use, T* raw_fill) -> bool {
-      MR_GLOBAL T* Rk = R(k);
+      // stage offsets as visibly wave-uniform values (SGPR soffsets, not per-lane waterfall loops)
+      const unsigned Rk = (unsigned)wu(w, (int)R(k));
       T eb[4], dq[4], dacl[4], ab;
       frag_finish(dd, raw_use, eb, dq, ab, dacl);
-      frag_load(R(k >= 1 ? k - 1 : 0), fp, raw_fill);  // unconditional: k = 0 re-reads its own record
+      frag_load(rb, (unsigned)wu(w, (int)R(k >= 2 ? k - 2 : 0)), fp, raw_fill);  // unconditional: k < 2 re-read stage 0's record
       // X = P^ E^  (A fragment s: P^[c][4s+g])
       // two independent 2-MFMA accumulation chains (k = 0..7 | 8..15) instead of one 4-long
       // dependent chain: half the MFMA latency on the stage's critical path
@@ -705,8 +715,8 @@ struct WaveSolver {
         const bool kcol = (g == 0) & (c < NX), kf0 = (g == 0) & (c == NX), kf1 = (g == 0) & (c == NX + 1);
 #pragma unroll
         for (int a = 0; a < NU; ++a) {
-          const int idx = kcol ? RCF::K + a * NX + c : (kf0 ? RCF::K0 + a : (kf1 ? RCF::K1 + a : RCF::JUNK));
-          Rk[idx] = kcol ? -kc[a] : (kf0 ? -k0[a] : -k1[a]);
+          const unsigned idx = kcol ? RCF::K + a * NX + c : (kf0 ? RCF::K0 + a : (kf1 ? RCF::K1 + a : RCF::JUNK));
+          rb.st(kcol ? -kc[a] : (kf0 ? -k0[a] : -k1[a]), Rk, idx);
         }
       }
       // closed-loop map (A + B K | B (k0 + mu k1) + c) for the forward recursion
@@ -717,25 +727,31 @@ struct WaveSolver {
 #pragma unroll
       for (int v = 0; v < 4; ++v) {  // branch-free: lanes without a target write their discard slot
         const T pv = dq[v] - dw[v];
-        Rk[fp.st_a[v]] = dacl[v];
-        Rk[fp.st_p[v]] = pv;
+        rb.st(dacl[v], Rk, (unsigned)fp.st_a[v]);
+        rb.st(pv, Rk, (unsigned)fp.st_p[v]);
         LP[fp.lp1[v]] = pv;
         LP[fp.lp2[v]] = pv;
       }
       wsync_lds(w);
       return piv_ok;
     };
-    // Pivots are tested once per stage pair, at the loop latch: a failed stage only costs the
-    // next one, and the loop keeps one back-edge block (exact prefetch waits at the loop head).
-    for (int k = N - 1;; k -= 2) {
-      bool ok = step(k, raw_a, raw_b);
+    // Pivots are tested once per three stages, at the loop latch: a failed stage only costs the
+    // next two, and the loop keeps one back-edge block (exact prefetch waits at the loop head).
+    // Buffer roles rotate a -> c -> b -> a over the three unrolled steps.
+    for (int k = N - 1;; k -= 3) {
+      bool ok = step(k, raw_a, raw_c);
       if (k == 0) {
         if (!wuni(w, ok)) return false;
         break;
       }
       ok = step(k - 1, raw_b, raw_a) & ok;
+      if (k == 1) {
+        if (!wuni(w, ok)) return false;
+        break;
+      }
+      ok = step(k - 2, raw_c, raw_b) & ok;
       if (!wuni(w, ok)) return false;
-      if (k == 1) break;
+      if (k == 2) break;
     }
     wsync(w);  // records (P, K, closed-loop map) visible to every lane
     return true;
@@ -756,11 +772,12 @@ struct WaveSolver {
     T dz[NZS];
     for (int i = 0; i < NZS; ++i) dz[i] = T(0);
     {
-      const int N = this->N, ln = this->ln;
+      const int N = wu(this->w, this->N), ln = this->ln;  // N wave-uniform: the stage offsets are soffsets
       const Wv w = this->w;
-      MR_GLOBAL T* const rcb = rc;
+      // the instance's workspace (stage fields, then the records) as one wave-uniform buffer
+      const WBuf<T> wb(rc - (int64_t)SSF::NF * WL, (unsigned)WS_WORDS);
+      auto R = [](int k) { return (unsigned)(SSF::NF * WL) + (unsigned)k * (unsigned)RC_STRIDE; };
       MR_LDS T* const LDX = lds + LDX_OFF;
-      auto R = [rcb](int k) { return rcb + (int64_t)k * RC_STRIDE; };
       // One recursion step per stage k = 0..N with three lane groups sharing the same dot product
       // row . dx_k (dx_k gathered from lanes 0..10): group 0 (lanes 0..10) row i of the closed-loop
       // map -> dx_{k+1}[i]; group 1 (lanes 16..26) row i of P_k -> the costate step
@@ -777,9 +794,17 @@ struct WaveSolver {
         roff[j] = g0r ? RCF::ACL + r * NX + j : (g1r ? RCF::P + pidx(r, j) : (g2r ? RCF::K + r * NX + j : RCF::CZERO));
       c0off = g0r ? RCF::FF + r : (g1r ? RCF::PV0 + r : (g2r ? RCF::K0 + r : RCF::CZERO));
       c1off = g1r ? RCF::PV1 + r : (g2r ? RCF::K1 + r : RCF::CZERO);
-      const int rnu = g1r ? r : 0;
-      MR_LDS T* const LDU = lds + LX_OFF;  // du_k[a] at [3 k + a] (the Riccati tiles are dead here)
+      const unsigned nuoff = (unsigned)(SSF::NU + (g1r ? r : 0)) * WL;
+      auto nu_ld = [&](int kk) -> T {
+        if constexpr (SSL) return ss[nuoff + kk];
+        else return wb.ld((unsigned)kk, nuoff);
+      };
       static_assert(3 * WL <= LP_OFF + 16 * LDS_LD, "du staging");
+      // LDS target of each lane's step result (branch-free, one store): group 0 dx_{k+1}[r] at
+      // LDX[(k + 1) 12 + r] (row N + 1 <= 64; N = 63: the discard slots), group 2 du_k[r] at
+      // [LX_OFF + 3 k + r] (the Riccati tiles are dead here), the others their discard slot
+      const int lbase = g0r ? LDX_OFF + 12 + r : (g2r ? LX_OFF + r : LJUNK_OFF + ln);
+      const int lstep = g0r ? 12 : (g2r ? 3 : 0);
       T dxi = T(0);
       if (ln < NX) LDX[ln] = T(0);
 #ifndef MR_FWD_PD
@@ -790,10 +815,10 @@ struct WaveSolver {
 #pragma unroll
       for (int d = 0; d < PD; ++d) {
         const int kk = d < N ? d : N;
-        for (int j = 0; j < NX; ++j) rw_r[d][j] = R(kk)[roff[j]];
-        c0_r[d] = R(kk)[c0off];
-        c1_r[d] = R(kk)[c1off];
-        nu_r[d] = ss[(SSF::NU + rnu) * WL + kk];
+        for (int j = 0; j < NX; ++j) rw_r[d][j] = wb.ld(R(kk), (unsigned)roff[j]);
+        c0_r[d] = wb.ld(R(kk), (unsigned)c0off);
+        c1_r[d] = wb.ld(R(kk), (unsigned)c1off);
+        nu_r[d] = nu_ld(kk);
       }
       for (int k0 = 0; k0 <= N; k0 += PD) {
 #pragma unroll
@@ -804,25 +829,42 @@ struct WaveSolver {
           for (int j = 0; j < NX; ++j) rw[j] = rw_r[d][j];
           const T c0 = c0_r[d], c1 = c1_r[d], nuv = nu_r[d];
           const int kn = k + PD < N ? k + PD : N;
-          for (int j = 0; j < NX; ++j) rw_r[d][j] = R(kn)[roff[j]];
-          c0_r[d] = R(kn)[c0off];
-          c1_r[d] = R(kn)[c1off];
-          nu_r[d] = ss[(SSF::NU + rnu) * WL + kn];
+          for (int j = 0; j < NX; ++j) rw_r[d][j] = wb.ld(R(kn), (unsigned)roff[j]);
+          c0_r[d] = wb.ld(R(kn), (unsigned)c0off);
+          c1_r[d] = wb.ld(R(kn), (unsigned)c1off);
+          nu_r[d] = nu_ld(kn);
           T dxv[NX];
           wgather<T, NX>(w, dxi, dxv);
+#if MR_FWD_TREE
+          // the 11-term dot as three interleaved chains (critical path 4 FMAs + 2 adds, not 11)
+          T a0 = c0 + mu * c1, a1 = rw[1] * dxv[1], a2 = rw[2] * dxv[2];
+          a0 += rw[0] * dxv[0];
+#pragma unroll
+          for (int j = 3; j < NX; j += 3) {
+            a0 += rw[j] * dxv[j];
+            if (j + 1 < NX) a1 += rw[j + 1] * dxv[j + 1];
+            if (j + 2 < NX) a2 += rw[j + 2] * dxv[j + 2];
+          }
+          const T acc = (a0 + a1) + a2;
+#else
           T acc = c0 + mu * c1;
           for (int j = 0; j < NX; ++j) acc += rw[j] * dxv[j];
+#endif
           dxi = g0r ? acc : T(0);
-          if (g0r) LDX[(k + 1) * 12 + r] = dxi;  // row N + 1 <= 64 (N = 63: the discard slots)
-          if (g1r && k >= 1) ss[(SSF::DNU + r) * WL + k] = acc - nuv;
-          if (g2r) LDU[3 * k + r] = acc;
+          lds[lbase + lstep * k] = acc;
+          const bool dn = g1r & (k >= 1);
+          if constexpr (SSL) {
+            if (dn) ss[(SSF::DNU + r) * WL + k] = acc - nuv;
+          } else {  // branch-free: other lanes write stage k's record discard slot
+            wb.st(acc - nuv, (unsigned)k, dn ? (unsigned)(SSF::DNU + r) * WL : R(k) + RCF::JUNK - (unsigned)k);
+          }
         }
       }
       wsync_lds(w);
       if (ln <= N)
         for (int j = 0; j < NX; ++j) dz[j] = LDX[ln * 12 + j];
       if (ln < N)
-        for (int a = 0; a < NU; ++a) dz[NX + a] = LDU[3 * ln + a];
+        for (int a = 0; a < NU; ++a) dz[NX + a] = lds[LX_OFF + 3 * ln + a];
     }
 #if MR_PHASE_CYCLES
     const unsigned long long tf1 = trace ? MR_CLOCK() : 0ull;
@@ -1032,7 +1074,14 @@ struct WaveSolver {
       MR_T0();
       for (int tries = 0; tries < 60; ++tries) {
         MR_CNT(6);
+#if MR_PHASE_CYCLES
+        const unsigned long long tr0 = trace ? MR_CLOCK() : 0ull;
+        const bool rok = riccati(delta, mu);
+        if (trace && !rok) { tsub[4] += MR_CLOCK() - tr0; tsub[5] += 1; }
+        if (rok) { fact_ok = true; break; }
+#else
         if (riccati(delta, mu)) { fact_ok = true; break; }
+#endif
         if (first) {
           delta = delta_last == T(0) ? T(1e-4) : mr_max(T(1e-20), delta_last / T(3));
           first = false;
@@ -1123,8 +1172,8 @@ struct WaveSolver {
       double* tr = trace + 8 * (trace_cap - 1);
       for (int q = 0; q < 7; ++q) tr[q] = (double)cyc[q];
       tr[7] = (double)(trace ? MR_CLOCK() - tstart : 0ull);
-      double* tr2 = trace + 8 * (trace_cap - 2);  // sub-phases: forward seq/par, eval stage/reduce
-      for (int q = 0; q < 4; ++q) tr2[q] = (double)tsub[q];
+      double* tr2 = trace + 8 * (trace_cap - 2);  // sub-phases: forward seq/par, eval stage/reduce, failed factorisations (cycles, count)
+      for (int q = 0; q < 6; ++q) tr2[q] = (double)tsub[q];
     }
 #endif
     if (trace && ln == 0 && it < trace_cap - 2) {

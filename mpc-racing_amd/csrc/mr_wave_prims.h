@@ -123,6 +123,36 @@ __device__ __forceinline__ MR_GLOBAL T* wu_gptr(MR_GLOBAL T* p) {
   return (MR_GLOBAL T*)(((unsigned long long)hi << 32) | lo);
 }
 
+// A wave-uniform global array addressed as (uniform word offset, per-lane word offset): a buffer
+// resource in SGPRs, so every access is one buffer_load / buffer_store with a 32-bit lane offset
+// VGPR and the uniform part in soffset -- no 64-bit per-lane address arithmetic, and no 64-bit
+// address VGPR pair per gathered word held across a loop.
+template <typename T>
+struct WBuf {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ WBuf(MR_GLOBAL T* base, unsigned n_words)
+      : r(__builtin_amdgcn_make_buffer_rsrc((void*)(T*)wu_gptr(base), 0, (int)(n_words * sizeof(T)), 0x00020000)) {}
+  __device__ __forceinline__ T ld(unsigned uoff, unsigned loff) const {
+    if constexpr (sizeof(T) == 4) {
+      return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)(loff * 4u), (int)(uoff * 4u), 0));
+    } else {
+      typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+      const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(loff * 8u), (int)(uoff * 8u), 0);
+      return __longlong_as_double((long long)(((unsigned long long)v[1] << 32) | v[0]));
+    }
+  }
+  __device__ __forceinline__ void st(T x, unsigned uoff, unsigned loff) const {
+    if constexpr (sizeof(T) == 4) {
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, (int)(loff * 4u), (int)(uoff * 4u), 0);
+    } else {
+      typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+      const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+      const u32x2 v = {(unsigned)b, (unsigned)(b >> 32)};
+      __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)(loff * 8u), (int)(uoff * 8u), 0);
+    }
+  }
+};
+
 // out[i] = value of lane i, i < n (compile-time n): one v_readlane per element
 template <typename T, int n>
 __device__ __forceinline__ void wgather(const Wv& w, T v, T* out) {
@@ -378,6 +408,14 @@ template <typename T>
 inline const T* wu_ptr(const T* p) { return p; }
 template <typename T>
 inline T* wu_gptr(T* p) { return p; }
+
+template <typename T>
+struct WBuf {
+  T* p;
+  WBuf(T* base, unsigned) : p(base) {}
+  T ld(unsigned uoff, unsigned loff) const { return p[uoff + loff]; }
+  void st(T x, unsigned uoff, unsigned loff) const { p[uoff + loff] = x; }
+};
 
 // host emulation of wtranspose4 (same result: lane (g, c) gets register g of lane (s, c))
 template <typename T>

@@ -12,7 +12,11 @@ for a in "$@"; do
   echo "$v $c rc=$rc"
   if [ $rc -ne 0 ]; then exit $rc; fi
 done
-if [ -f variants/lib_cyc.so ]; then
-  MR_PRODUCT_LIB=variants/lib_cyc.so timeout -k 10 300 python -u mpc-racing_amd/tools/phase_probe.py C4 > gpurun_out/phase_cyc.log 2>&1
-  echo "phase rc=$?"
-fi
+for lib in variants/lib_cyc*.so; do
+  [ -f "$lib" ] || continue
+  v=$(basename "$lib" .so); v=${v#lib_}
+  MR_PRODUCT_LIB=$lib timeout -k 10 300 python -u mpc-racing_amd/tools/phase_probe.py C4 > gpurun_out/phase_$v.log 2>&1
+  rc=$?
+  echo "phase $v rc=$rc"
+  if [ $rc -ne 0 ]; then exit $rc; fi
+done

@@ -40,7 +40,7 @@ def one(name, b, i, cap=520):
     tr = out["trace"].cpu().numpy()
     it = int(out["iters"][0])
     row = dict(zip(NAMES, tr[-1].tolist()))
-    row.update(dict(zip(["fwd_seq", "fwd_par", "eval_stage", "eval_reduce"], tr[-2][:4].tolist())))
+    row.update(dict(zip(["fwd_seq", "fwd_par", "eval_stage", "eval_reduce", "fact_failed_cycles", "n_fact_failed"], tr[-2][:6].tolist())))
     row.update(instance=i, iters=it, status=int(out["status"][0]), wall_ms=1e3 * min(lat),
                cycles_per_iter=row["total"] / max(it, 1))
     return row
