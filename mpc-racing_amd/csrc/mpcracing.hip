@@ -110,39 +110,63 @@ __global__ __launch_bounds__(WL, sizeof(T) == 4 ? MR_WAVES_PER_SIMD_F32 : MR_WAV
   }
 }
 
-// Dispatch order (mr_config.dispatch_order = 1): a stable partition of the batch putting first the
-// instances whose initial speed is near the ends of the sampled range -- through the 15 m/s blend
-// corner, or fast enough that the contouring problem is hardest -- which are the ones that run
-// hundreds of iterations (profiles/r02_tail_audit.json).  Workgroups are dispatched roughly in
-// index order, so these long solves start early instead of extending the batch.  One workgroup of
-// 1024 threads: per-thread chunk counts, an LDS scan, then every thread writes its chunk.
+// Dispatch order (mr_config.dispatch_order = 1): a stable three-tier partition of the batch so that
+// the solves likely to run hundreds of iterations start first -- workgroups are dispatched roughly
+// in index order, and a long solve that starts late extends the batch (profiles/r02_C4_timeline_*).
+//   tier 0: near the top speed (v >= 40 m/s), or under hard braking (throttle0 <= -0.5) at v <= 20 m/s:
+//           with the throttle rate limit the predicted car decelerates through a blend corner of the
+//           model (Vblendmax = 15 m/s, Vblendmin = 2 m/s, models/VehicleParameters.py:37-38) within the
+//           horizon -- 23 % of C4 (fits the first dispatch round), 26 of its 30 solves >= 300 iterations;
+//   tier 1: the other instances outside 16.5 < v < 39 (the Vblendmax = 15 m/s blend corner nearby,
+//           or fast);
+//   tier 2: the rest.
+// One workgroup of 1024 threads: per-thread chunk counts per tier, two LDS scans, then every thread
+// writes its chunk.  NaN speeds go to tier 0.
 constexpr int kOrderThreads = 1024;
-__global__ __launch_bounds__(kOrderThreads) void mr_order_kernel(const double* state0, int B, int* order) {
-  __shared__ int cnt[kOrderThreads];
-  const int t = threadIdx.x;
-  const int per = (B + kOrderThreads - 1) / kOrderThreads;
-  const int lo = min(B, t * per), hi = min(B, lo + per);
-  auto prio = [&](int i) {
-    const double vx = state0[3 * (int64_t)B + i], vy = state0[4 * (int64_t)B + i];
-    const double v = sqrt(vx * vx + vy * vy);
-    return !(v > 16.5 && v < 39.0);  // NaN speeds go first too
-  };
-  int c = 0;
-  for (int i = lo; i < hi; ++i) c += prio(i) ? 1 : 0;
+__device__ __forceinline__ int order_tier(const double* state0, int B, int i) {
+  const double vx = state0[3 * (int64_t)B + i], vy = state0[4 * (int64_t)B + i], thr = state0[6 * (int64_t)B + i];
+  const double v = sqrt(vx * vx + vy * vy);
+  if (!(v < 40.0) || (v <= 20.0 && thr <= -0.5)) return 0;
+  return (v > 16.5 && v < 39.0) ? 2 : 1;
+}
+__device__ __forceinline__ int order_scan(int* cnt, int t, int c) {  // inclusive scan of c over the block
   cnt[t] = c;
   __syncthreads();
-  for (int off = 1; off < kOrderThreads; off <<= 1) {  // inclusive scan (Hillis-Steele)
+  for (int off = 1; off < kOrderThreads; off <<= 1) {  // Hillis-Steele
     const int v = t >= off ? cnt[t - off] : 0;
     __syncthreads();
     cnt[t] += v;
     __syncthreads();
   }
-  const int total = cnt[kOrderThreads - 1];
-  int pa = cnt[t] - c;            // priority slots before this chunk
-  int pb = total + (lo - pa);     // the others after all priority ones, stable
+  const int r = cnt[t];
+  __syncthreads();
+  return r;
+}
+__global__ __launch_bounds__(kOrderThreads) void mr_order_kernel(const double* state0, int B, int* order) {
+  __shared__ int cnt[kOrderThreads];
+  __shared__ int tot[2];
+  const int t = threadIdx.x;
+  const int per = (B + kOrderThreads - 1) / kOrderThreads;
+  const int lo = min(B, t * per), hi = min(B, lo + per);
+  int c0 = 0, c1 = 0;
   for (int i = lo; i < hi; ++i) {
-    if (prio(i)) order[pa++] = i;
-    else order[pb++] = i;
+    const int q = order_tier(state0, B, i);
+    c0 += q == 0;
+    c1 += q == 1;
+  }
+  const int s0 = order_scan(cnt, t, c0);
+  if (t == kOrderThreads - 1) tot[0] = s0;
+  const int s1 = order_scan(cnt, t, c1);
+  if (t == kOrderThreads - 1) tot[1] = s1;
+  __syncthreads();
+  int p0 = s0 - c0;                          // tier-0 slots before this chunk
+  int p1 = tot[0] + (s1 - c1);               // tier 1 after all of tier 0
+  int p2 = tot[0] + tot[1] + (lo - (s0 - c0) - (s1 - c1));  // tier 2 after both
+  for (int i = lo; i < hi; ++i) {
+    const int q = order_tier(state0, B, i);
+    if (q == 0) order[p0++] = i;
+    else if (q == 1) order[p1++] = i;
+    else order[p2++] = i;
   }
 }
 

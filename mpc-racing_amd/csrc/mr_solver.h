@@ -433,6 +433,12 @@ struct SolveOut {
 #ifndef MR_FMAX
 #define MR_FMAX 16
 #endif
+#ifndef MR_FILTER_RESET_TRIGGER
+#define MR_FILTER_RESET_TRIGGER 5  // IPOPT filter_reset_trigger (0: heuristic off)
+#endif
+#ifndef MR_MAX_FILTER_RESETS
+#define MR_MAX_FILTER_RESETS 5  // IPOPT max_filter_resets
+#endif
 #ifndef MR_LS_FAIL_MAX
 #define MR_LS_FAIL_MAX 1000000
 #endif
@@ -1018,6 +1024,9 @@ struct Solver {
     T mu_prev = mu;
     int acc_count = 0;
     int ls_fail = 0;  // consecutive iterations without an acceptable line-search step
+    // IPOPT's filter reset heuristic (filter_reset_trigger = 5, max_filter_resets = 5): after this many
+    // successive iterations whose line search had a trial point rejected by the filter, clear it
+    int filt_rej_iters = 0, filt_resets = 0;
     int it = 0;
     for (it = 0;; ++it) {
       MR_PROF(0, eval_sweep(mu_prev));
@@ -1077,7 +1086,7 @@ struct Solver {
         a_min = T(0.05) * g_th;
       }
       T alpha = ap;
-      bool accepted = false, ftype = false;
+      bool accepted = false, ftype = false, rej_filter = false;
       int nls = 0;
       // backtracking ends below a_min, or below 1e-30: a_min is 0 when theta is (and may flush to 0
       // in fp32), and halving alpha to 0 would never leave the loop
@@ -1087,7 +1096,7 @@ struct Solver {
           T th_t, ph_t;
           bool ok;
           MR_PROF(3, ok = trial(alpha, soc, th_t, ph_t));
-          if (ok) ok = th_t <= theta_max && filter_ok(th_t, ph_t);
+          if (ok) ok = th_t <= theta_max;
           if (ok) {
             bool sw = gphi < T(0) && alpha * mr_exp(s_phi * mr_log(-gphi)) > delta_sw * th_pow;
             if (th <= theta_min && sw) {
@@ -1098,6 +1107,9 @@ struct Solver {
               ftype = false;
             }
           }
+          // the filter last (IPOPT's order: theta_max, sufficient decrease, then the filter), so a
+          // rejection by the filter itself is known for the reset heuristic
+          if (ok && !filter_ok(th_t, ph_t)) { ok = false; rej_filter = true; }
           if (ok) { accepted = true; break; }
           // second-order correction only after the first rejected trial with theta not decreased
           if (!(nls == 0 && !soc && th_t >= th)) break;
@@ -1115,6 +1127,16 @@ struct Solver {
         trial(alpha, false, th_t, ph_t);
         ftype = false;
       }
+#if MR_FILTER_RESET_TRIGGER > 0
+      if (filt_resets < MR_MAX_FILTER_RESETS) {
+        filt_rej_iters = rej_filter ? filt_rej_iters + 1 : 0;
+        if (filt_rej_iters >= MR_FILTER_RESET_TRIGGER) {
+          nfilt = 0;
+          filt_resets++;
+          filt_rej_iters = 0;
+        }
+      }
+#endif
       if (!ftype) filter_add((T(1) - g_th) * th, ph - g_ph * th);
       if (trace && it < trace_cap) {
         double* tr = trace + 8 * it;

@@ -61,6 +61,9 @@
 #ifndef MR_PHASE_CYCLES
 #define MR_PHASE_CYCLES 0  // 1: per-sweep shader-cycle counters of the trace instance (tools/phase_probe.py)
 #endif
+#ifndef MR_EVAL_HOIST
+#define MR_EVAL_HOIST 0  // 1: the evaluation sweep loads slacks / multipliers ahead of the record stores
+#endif
 #ifndef MR_FWD_TREE
 #define MR_FWD_TREE 0  // 1: the forward recursion's dot products as three chains (A/B option)
 #endif
@@ -363,6 +366,16 @@ struct WaveSolver {
     }
     T z[NZS];
     load_z(cur, z);
+#if MR_EVAL_HOIST
+    // the slacks and multipliers of every row loaded with the iterate, ahead of the record stores
+    // (otherwise the compiler must keep them behind those stores: a second memory round trip)
+    T s_in[NI], lam_in[NI], dlam_in[NI];
+    for (int j = 0; j < NI; ++j) {
+      s_in[j] = own() ? S(sf(cur) + j) : T(1);
+      lam_in[j] = own() ? S(SSF::LAM + j) : T(0);
+      dlam_in[j] = own() ? S(SSF::DLAM + j) : T(0);
+    }
+#endif
     T nun[NX], znext[NX];
     for (int i = 0; i < NX; ++i) {
       nun[i] = wshfl(w, nuk[i], nxt());
@@ -416,8 +429,13 @@ struct WaveSolver {
         lam_j[j] = T(0);
         s_j[j] = T(1);
         if (!act[j]) continue;
+#if MR_EVAL_HOIST
+        T s = s_in[j];
+        T lam = lam_in[j] + alpha_d * dlam_in[j];
+#else
         T s = S(sf(cur) + j);
         T lam = S(SSF::LAM + j) + alpha_d * S(SSF::DLAM + j);
+#endif
         lam = mr_min(mr_max(lam, mu_prev / (kappa_sigma * s)), kappa_sigma * mu_prev / s);
         S(SSF::LAM + j) = lam;
         lam_j[j] = lam;
@@ -1031,6 +1049,9 @@ struct WaveSolver {
     T mu_prev = mu;
     int acc_count = 0;
     int ls_fail = 0;  // consecutive iterations without an acceptable line-search step
+    // IPOPT's filter reset heuristic (filter_reset_trigger = 5, max_filter_resets = 5): after this many
+    // successive iterations whose line search had a trial point rejected by the filter, clear it
+    int filt_rej_iters = 0, filt_resets = 0;
     int it = 0;
     // diagnostics of the trace instance: shader cycles per phase and call counts (MR_PHASE_CYCLES
     // builds only -- the counters stay live across every sweep call, so the product build has none)
@@ -1108,7 +1129,7 @@ struct WaveSolver {
         a_min = T(0.05) * g_th;
       }
       T alpha = ap;
-      bool accepted = false, ftype = false;
+      bool accepted = false, ftype = false, rej_filter = false;
       int nls = 0;
       // backtracking ends below a_min, or below 1e-30: a_min is 0 when theta is (and may flush to 0
       // in fp32), and halving alpha to 0 would never leave the loop
@@ -1121,7 +1142,7 @@ struct WaveSolver {
           MR_T1(3);
           MR_CNT(4);
           if (soc) MR_CNT(5);
-          if (ok) ok = th_t <= theta_max && filter_ok(th_t, ph_t);
+          if (ok) ok = th_t <= theta_max;
           if (ok) {
             bool sw = gphi < T(0) && alpha * mr_exp(s_phi * mr_log(-gphi)) > delta_sw * th_pow;
             if (th <= theta_min && sw) {
@@ -1132,6 +1153,9 @@ struct WaveSolver {
               ftype = false;
             }
           }
+          // the filter last (IPOPT's order: theta_max, sufficient decrease, then the filter), so a
+          // rejection by the filter itself is known for the reset heuristic
+          if (ok && !filter_ok(th_t, ph_t)) { ok = false; rej_filter = true; }
           if (ok) { accepted = true; break; }
           if (!(nls == 0 && !soc && th_t >= th)) break;
         }
@@ -1151,6 +1175,16 @@ struct WaveSolver {
         trial(alpha, false, th_t, ph_t);
         ftype = false;
       }
+#if MR_FILTER_RESET_TRIGGER > 0
+      if (filt_resets < MR_MAX_FILTER_RESETS) {
+        filt_rej_iters = rej_filter ? filt_rej_iters + 1 : 0;
+        if (filt_rej_iters >= MR_FILTER_RESET_TRIGGER) {
+          nfilt = 0;
+          filt_resets++;
+          filt_rej_iters = 0;
+        }
+      }
+#endif
       if (!ftype) filter_add((T(1) - g_th) * th, ph - g_ph * th);
       if (trace && ln == 0 && it < trace_cap - 2) {
         double* tr = trace + 8 * it;

@@ -123,6 +123,12 @@ __device__ __forceinline__ MR_GLOBAL T* wu_gptr(MR_GLOBAL T* p) {
   return (MR_GLOBAL T*)(((unsigned long long)hi << 32) | lo);
 }
 
+// the same for either address space: global pointers through readfirstlane, LDS ones unchanged
+template <typename T>
+__device__ __forceinline__ MR_GLOBAL T* wu_any(MR_GLOBAL T* p) { return wu_gptr(p); }
+template <typename T>
+__device__ __forceinline__ MR_LDS T* wu_any(MR_LDS T* p) { return p; }
+
 // A wave-uniform global array addressed as (uniform word offset, per-lane word offset): a buffer
 // resource in SGPRs, so every access is one buffer_load / buffer_store with a 32-bit lane offset
 // VGPR and the uniform part in soffset -- no 64-bit per-lane address arithmetic, and no 64-bit
@@ -408,6 +414,8 @@ template <typename T>
 inline const T* wu_ptr(const T* p) { return p; }
 template <typename T>
 inline T* wu_gptr(T* p) { return p; }
+template <typename T>
+inline T* wu_any(T* p) { return p; }
 
 template <typename T>
 struct WBuf {

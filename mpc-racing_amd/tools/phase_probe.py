@@ -57,7 +57,21 @@ def main():
         it = o["iters"]
         order = np.argsort(it)
         picks = [int(order[len(order) // 2]), int(order[-1]), int(order[-2])]
+        if len(sys.argv) > 2:  # explicit instances: python phase_probe.py C4 395,4387
+            picks = [int(x) for x in sys.argv[2].split(",")]
         res[name] = [one(name, b, i) for i in picks]
+        # the same instances traced inside the full batch launch (memory system and SIMD shared with
+        # the other 8 191 solves): which phases the contention slows
+        for i in picks:
+            o = s.solve(b, trace_instance=i, trace_cap=520)
+            tr = o["trace"].cpu().numpy()
+            it_i = int(o["iters"][i])
+            row = dict(zip(NAMES, tr[-1].tolist()))
+            row.update(dict(zip(["fwd_seq", "fwd_par", "eval_stage", "eval_reduce", "fact_failed_cycles",
+                                 "n_fact_failed"], tr[-2][:6].tolist())))
+            row.update(instance=i, iters=it_i, status=int(o["status"][i]), in_batch=True,
+                       cycles_per_iter=row["total"] / max(it_i, 1))
+            res[name].append(row)
         for r in res[name]:
             print(name, json.dumps(r), flush=True)
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)

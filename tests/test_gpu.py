@@ -276,3 +276,14 @@ def test_c4_fp64_gpu_vs_host_statuses():
     print("host status", h["status"].tolist(), "iters", h["iters"].tolist())
     print("gpu kkt", o["kkt"].tolist())
     assert (o["status"] == h["status"]).all()
+
+
+def test_dispatch_order_does_not_change_results():
+    """mr_config.dispatch_order = 1 (the three-tier long-solves-first permutation of the workgroups,
+    mr_order_kernel) must give bit-identical outputs to index order: every instance solved exactly once,
+    by the same code, on the same inputs."""
+    b = wl.make_batch("C4", limit=3000)  # not a multiple of the order kernel's 1024 threads
+    o0 = _np(solver_for_config("C4", 3000, dispatch_order=0).solve(b))
+    o1 = _np(solver_for_config("C4", 3000, dispatch_order=1).solve(b))
+    for k in o0:
+        assert np.array_equal(o0[k], o1[k]), k
