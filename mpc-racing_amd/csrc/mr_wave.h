@@ -210,7 +210,8 @@ struct WaveSolver {
   int me, mi;
   // out-parameters of the non-inlined sweeps: members, so they land in the object's LDS slot
   // rather than in the caller's private stack (a scratch round trip after every call)
-  T res_ap, res_ad, res_gphi, res_th, res_ph;
+  T res_ap, res_ad, res_gphi, res_alpha;
+  int res_flags, res_nls, res_ntr, res_nsoc;
   double* trace = nullptr;
   int trace_cap = 0;
 #if MR_PHASE_CYCLES
@@ -941,78 +942,158 @@ struct WaveSolver {
 #endif
   }
 
-  // ---------------- sweep 4: line-search trial point (writes buffer 1-cur) ----------------
-  MR_SWEEP bool trial(T alpha, bool soc, T& th_t, T& ph_t) {
+  // ---------------- sweep 4: the filter line search (IPOPT backtracking, one SOC) ----------------
+  // The lane's stage iterate, step, slacks and slack steps are loaded once; every trial point is
+  // formed and measured in registers (one pass per trial: the trial's stage values, its dynamics
+  // defect against the neighbour's trial state, three wave sums), and only the accepted point --
+  // or the fallback point when none is acceptable -- is written to iterate buffer 1-cur.
+  // Backtracking (same rules and order as IPOPT's filter line search, Waechter & Biegler 2006):
+  // alpha = ap, ap/2, ... down to a_min; a second-order correction only after the first trial
+  // (nls = 0) when it did not decrease theta; acceptance = theta_max, then the switching /
+  // Armijo or sufficient-decrease test, then the filter.
+  MR_SWEEP void line_search(T th, T ph, T gphi, T ap, T a_min, T th_pow) {
     MR_UNIFORM_P();
     MR_ASSUME_LDS_STATE();
+    const T s_phi = T(2.3), delta_sw = T(1), eta = T(1e-4), g_th = T(1e-5), g_ph = T(1e-5);
     const int nb = 1 - cur;
     const int k = ln;
-    T z[NZS], zt[NZS], zpl[NZS];
+    T z[NZS], dz[NZS], s_c[NI], ds[NI];
     load_z(cur, z);
-    for (int i = 0; i < NZS; ++i) zt[i] = z[i] + alpha * (own() ? S(SSF::DZ + i) : T(0));
-    if (k == 0)
-      for (int i = 0; i < NX; ++i) zt[i] = z[i];  // x_0 fixed
-    if (k >= N) { zt[11] = zt[12] = zt[13] = T(0); }
-    for (int i = 0; i < NZS; ++i) zpl[i] = zt[i];
-    if (soc) {
-      // second-order correction: re-roll the shooting states through the dynamics (sequential)
-      T xr[NX], myx[NX];
-      for (int i = 0; i < NX; ++i) { xr[i] = wbcast(w, z[i], 0); myx[i] = xr[i]; }
-      for (int kk = 0; kk < N; ++kk) {
-        T zz[NZS];
-        for (int i = 0; i < NX; ++i) zz[i] = xr[i];
-        zz[11] = wbcast(w, zpl[11], kk);
-        zz[12] = wbcast(w, zpl[12], kk);
-        zz[13] = wbcast(w, zpl[13], kk);
-        zz[14] = T(0);
-        T xn[NX];
-        faug<T, MODEL>(P, kk, zz, xn);
-        for (int i = 0; i < NX; ++i) xr[i] = xn[i];
-        if (ln == kk + 1)
-          for (int i = 0; i < NX; ++i) myx[i] = xr[i];
-      }
-      if (k >= 1)
-        for (int i = 0; i < NX; ++i) zt[i] = myx[i];
+    for (int i = 0; i < NZS; ++i) dz[i] = own() ? S(SSF::DZ + i) : T(0);
+    unsigned actm = 0u;  // active rows of this stage (depend on the stage only, not on the point)
+#pragma unroll
+    for (int r = 0; r < NROW; ++r) {
+      int a;
+      T lo, hi;
+      row_bounds(P, I, k, r, a, lo, hi);
+      actm |= (own() && a) ? (3u << (2 * r)) : 0u;
     }
-    T ztn[NX];
-    for (int i = 0; i < NX; ++i) ztn[i] = wshfl(w, zt[i], nxt());
-    T th_l = T(0), f_l = T(0), lg_l = T(0);
-    int ok_l = 1;
-    if (own()) {
-      Err<T> e, ep;
-      errors(I, zt[0], zt[1], zt[6], e, false);
-      T d[NI], dp[NI];
-      int act[NI];
-      row_values(k, zt, e, d, act);
+    actm |= (own() && lane_active(P, k)) ? (7u << JL) : 0u;
+    for (int j = 0; j < NI; ++j) {
+      const bool a = (actm >> j) & 1u;
+      s_c[j] = a ? S(sf(cur) + j) : T(1);
+      ds[j] = a ? S(SSF::DS + j) : T(0);
+    }
+    T zt[NZS], st[NI];
+    // one trial point: zt, st (registers), theta, phi; false if a slack is not positive or a value is
+    // not finite
+    auto eval = [&](T alpha, bool soc, T& th_t, T& ph_t) -> bool {
+      for (int i = 0; i < NZS; ++i) zt[i] = z[i] + alpha * dz[i];
+      if (k == 0)
+        for (int i = 0; i < NX; ++i) zt[i] = z[i];  // x_0 fixed
+      if (k >= N) { zt[11] = zt[12] = zt[13] = T(0); }
+      T zpl[NZS];
+      for (int i = 0; i < NZS; ++i) zpl[i] = zt[i];
       if (soc) {
-        errors(I, zpl[0], zpl[1], zpl[6], ep, false);
-        int actp[NI];
-        row_values(k, zpl, ep, dp, actp);
+        // second-order correction: re-roll the shooting states through the dynamics (sequential)
+        T xr[NX], myx[NX];
+        for (int i = 0; i < NX; ++i) { xr[i] = wbcast(w, z[i], 0); myx[i] = xr[i]; }
+        for (int kk = 0; kk < N; ++kk) {
+          T zz[NZS];
+          for (int i = 0; i < NX; ++i) zz[i] = xr[i];
+          zz[11] = wbcast(w, zpl[11], kk);
+          zz[12] = wbcast(w, zpl[12], kk);
+          zz[13] = wbcast(w, zpl[13], kk);
+          zz[14] = T(0);
+          T xn[NX];
+          faug<T, MODEL>(P, kk, zz, xn);
+          for (int i = 0; i < NX; ++i) xr[i] = xn[i];
+          if (ln == kk + 1)
+            for (int i = 0; i < NX; ++i) myx[i] = xr[i];
+        }
+        if (k >= 1)
+          for (int i = 0; i < NX; ++i) zt[i] = myx[i];
       }
-      for (int j = 0; j < NI; ++j) {
-        if (!act[j]) continue;
-        T st = S(sf(cur) + j) + alpha * S(SSF::DS + j);
-        if (soc) st += d[j] - dp[j];
-        if (!(st > T(0))) ok_l = 0;
-        S(sf(nb) + j) = st;
-        th_l += mr_abs(d[j] - st);
-        lg_l += mr_log(st > T(0) ? st : T(1));
+      T ztn[NX];
+      for (int i = 0; i < NX; ++i) ztn[i] = wshfl(w, zt[i], nxt());
+      T th_l = T(0), f_l = T(0), lg_l = T(0);
+      int ok_l = 1;
+      if (own()) {
+        Err<T> e, ep;
+        errors(I, zt[0], zt[1], zt[6], e, false);
+        T d[NI], dp[NI];
+        int act[NI];
+        row_values(k, zt, e, d, act);
+        if (soc) {
+          errors(I, zpl[0], zpl[1], zpl[6], ep, false);
+          int actp[NI];
+          row_values(k, zpl, ep, dp, actp);
+        }
+        for (int j = 0; j < NI; ++j) {
+          st[j] = s_c[j];
+          if (!((actm >> j) & 1u)) continue;
+          T sj = s_c[j] + alpha * ds[j];
+          if (soc) sj += d[j] - dp[j];
+          if (!(sj > T(0))) ok_l = 0;
+          st[j] = sj;
+          th_l += mr_abs(d[j] - sj);
+          lg_l += mr_log(sj > T(0) ? sj : T(1));
+        }
+        f_l += stage_cost(P, I, k, zt, e, sc, (T*)nullptr, (T*)nullptr);
+        if (lane_active(P, k)) f_l += sc * P.lane_pen * zt[14];
+        if (k < N && !soc) {
+          T xn[NX];
+          faug<T, MODEL>(P, k, zt, xn);
+          for (int i = 0; i < NX; ++i) th_l += mr_abs(xn[i] - ztn[i]);
+        }
       }
-      f_l += stage_cost(P, I, k, zt, e, sc, (T*)nullptr, (T*)nullptr);
-      if (lane_active(P, k)) f_l += sc * P.lane_pen * zt[14];
-      if (k < N && !soc) {
-        T xn[NX];
-        faug<T, MODEL>(P, k, zt, xn);
-        for (int i = 0; i < NX; ++i) th_l += mr_abs(xn[i] - ztn[i]);
+      th_t = wsum(w, th_l);
+      const T fv = wsum(w, f_l), lg = wsum(w, lg_l);
+      int ok = wmin(w, ok_l);
+      ph_t = fv - mu * lg;
+      if (!(th_t == th_t) || !(ph_t == ph_t)) ok = 0;
+      return wuni(w, ok != 0);
+    };
+    T alpha = ap;
+    int nls = 0, pass = 0, ntr = 0, nsoc = 0;
+    bool accepted = false, ftype = false, rej_filter = false;
+    // backtracking ends below a_min, or below 1e-30: a_min is 0 when theta is (and may flush to 0 in
+    // fp32), and halving alpha to 0 would never leave the loop.  No acceptable step: IPOPT would enter
+    // its restoration phase; this solver takes the shortest tried step (never past the
+    // fraction-to-boundary step, so the slacks stay positive) -- the fallback point.
+    bool fallback = !(alpha >= a_min && alpha >= T(1e-30));
+    if (fallback) alpha = mr_min(mr_max(alpha, a_min), ap);
+    for (;;) {
+      const bool soc = pass == 1;
+      T th_t, ph_t;
+      bool ok = eval(alpha, soc, th_t, ph_t);
+      ntr++;
+      nsoc += soc ? 1 : 0;
+      if (fallback) { ftype = false; break; }
+      if (ok) ok = th_t <= theta_max;
+      if (ok) {
+        const bool sw = gphi < T(0) && alpha * mr_exp(s_phi * mr_log(-gphi)) > delta_sw * th_pow;
+        if (th <= theta_min && sw) {
+          ok = ph_t <= ph + eta * alpha * gphi + T(1e-14) * mr_abs(ph);
+          ftype = true;
+        } else {
+          ok = th_t <= (T(1) - g_th) * th || ph_t <= ph - g_ph * th + T(1e-14) * mr_abs(ph);
+          ftype = false;
+        }
       }
+      // the filter last (IPOPT's order), so a rejection by the filter itself is known for the reset
+      // heuristic
+      if (ok && !filter_ok(th_t, ph_t)) { ok = false; rej_filter = true; }
+      if (wuni(w, ok)) { accepted = true; break; }
+      if (pass == 0 && nls == 0 && th_t >= th) { pass = 1; continue; }  // second-order correction
+      pass = 0;
+      alpha *= T(0.5);
+      nls++;
+      if (!(alpha >= a_min && alpha >= T(1e-30))) {
+        fallback = true;
+        alpha = mr_min(mr_max(alpha, a_min), ap);
+      }
+    }
+    if (own()) {  // the chosen point
+      for (int j = 0; j < NI; ++j)
+        if ((actm >> j) & 1u) S(sf(nb) + j) = st[j];
       for (int i = 0; i < NZS; ++i) S(zf(nb) + i) = zt[i];
     }
-    th_t = wsum(w, th_l);
-    T fv = wsum(w, f_l), lg = wsum(w, lg_l);
-    int ok = wmin(w, ok_l);
-    ph_t = fv - mu * lg;
-    if (!(th_t == th_t) || !(ph_t == ph_t)) ok = 0;
-    return ok != 0;
+    res_alpha = alpha;
+    res_flags = (accepted ? 1 : 0) | (ftype ? 2 : 0) | (rej_filter ? 4 : 0);
+    res_nls = nls;
+    res_ntr = ntr;
+    res_nsoc = nsoc;
   }
 
   MR_HD bool filter_ok(T th, T ph) const {
@@ -1128,53 +1209,20 @@ struct WaveSolver {
       } else {
         a_min = T(0.05) * g_th;
       }
-      T alpha = ap;
-      bool accepted = false, ftype = false, rej_filter = false;
-      int nls = 0;
-      // backtracking ends below a_min, or below 1e-30: a_min is 0 when theta is (and may flush to 0
-      // in fp32), and halving alpha to 0 would never leave the loop
-      while (alpha >= a_min && alpha >= T(1e-30)) {
-        for (int pass = 0; pass < 2 && !accepted; ++pass) {
-          bool soc = pass == 1;
-          T &th_t = res_th, &ph_t = res_ph;
-          MR_T0();
-          bool ok = trial(alpha, soc, th_t, ph_t);
-          MR_T1(3);
-          MR_CNT(4);
-          if (soc) MR_CNT(5);
-          if (ok) ok = th_t <= theta_max;
-          if (ok) {
-            bool sw = gphi < T(0) && alpha * mr_exp(s_phi * mr_log(-gphi)) > delta_sw * th_pow;
-            if (th <= theta_min && sw) {
-              ok = ph_t <= ph + eta * alpha * gphi + T(1e-14) * mr_abs(ph);
-              ftype = true;
-            } else {
-              ok = th_t <= (T(1) - g_th) * th || ph_t <= ph - g_ph * th + T(1e-14) * mr_abs(ph);
-              ftype = false;
-            }
-          }
-          // the filter last (IPOPT's order: theta_max, sufficient decrease, then the filter), so a
-          // rejection by the filter itself is known for the reset heuristic
-          if (ok && !filter_ok(th_t, ph_t)) { ok = false; rej_filter = true; }
-          if (ok) { accepted = true; break; }
-          if (!(nls == 0 && !soc && th_t >= th)) break;
-        }
-        if (accepted) break;
-        alpha *= T(0.5);
-        nls++;
-      }
-      // No acceptable step: IPOPT would enter its feasibility restoration phase; this solver has
-      // none.  It takes the shortest tried step (never past the fraction-to-boundary step, so the
-      // slacks stay positive) and, after MR_LS_FAIL_MAX consecutive failures, stops with status
-      // failed -- IPOPT's "restoration failed" outcome -- instead of spinning to max_iter.
+      MR_T0();
+      line_search(th, ph, gphi, ap, a_min, th_pow);
+      MR_T1(3);
+#if MR_PHASE_CYCLES
+      cyc[4] += res_ntr;
+      cyc[5] += res_nsoc;
+#endif
+      const T alpha = res_alpha;
+      const bool accepted = res_flags & 1, ftype = res_flags & 2, rej_filter = res_flags & 4;
+      const int nls = res_nls;
+      // after MR_LS_FAIL_MAX consecutive iterations without an acceptable step the solve stops with
+      // status failed (IPOPT's "restoration failed" outcome) instead of spinning to max_iter
       ls_fail = accepted ? 0 : ls_fail + 1;
       if (ls_fail >= MR_LS_FAIL_MAX) { out.status = 3; break; }
-      if (!accepted) {
-        alpha = mr_min(mr_max(alpha, a_min), ap);
-        T &th_t = res_th, &ph_t = res_ph;
-        trial(alpha, false, th_t, ph_t);
-        ftype = false;
-      }
 #if MR_FILTER_RESET_TRIGGER > 0
       if (filt_resets < MR_MAX_FILTER_RESETS) {
         filt_rej_iters = rej_filter ? filt_rej_iters + 1 : 0;
