@@ -85,12 +85,12 @@ struct RCF {
   enum {
     J = 0, C = J + 48, H = C + NX, G0 = H + NH, G1 = G0 + NZ,
     P = G1 + NZ, PV0 = P + NP,
-    PV1 = PV0 + NX, K = PV1 + NX, K0 = K + NU * NX, K1 = K0 + NU, ACL = K1 + NU, FF = ACL + NX * NX,
-    CONE = FF + NX, CZERO, SELP, SEL0,  // constants 1, 0, [k > 0], [k == 0] (written once per solve)
+    PV1 = PV0 + NX, K = PV1 + NX, K0 = K + NU * NX, K1 = K0 + NU,
+    CONE = K1 + NU, CZERO, SELP, SEL0,  // constants 1, 0, [k > 0], [k == 0] (written once per solve)
     JUNK, NF                           // discard slot of the branch-free stores (any lane)
   };
 };
-constexpr int RC_STRIDE = 480;  // words; 16-word (64 B) multiple
+constexpr int RC_STRIDE = 336;  // words; 16-word (64 B) multiple
 static_assert(RCF::NF <= RC_STRIDE, "record");
 constexpr int64_t WS_WORDS = (int64_t)SSF::NF * WL + (int64_t)RC_STRIDE * WL;
 constexpr int LDS_LD = 17;  // padded row of the 16 x 16 LDS tiles
@@ -555,49 +555,46 @@ struct WaveSolver {
 
   // Per-lane MFMA operands of stage k (lane = (g, c) = (lane >> 4, lane & 15)):
   //   eb[s] = E^[4s+g][c]                           B fragment of X = P^ E^ and A fragment of E^T X
-  //   ab    = B[c][g] = E^[c][11+g]                 A fragment of B K
   //   hc[v] = (H + delta I | g0 | g1)[drow(g,v)][c]  C input of Q
-  //   ac[v] = (A | 0 | c)[drow(g,v)][c]             C input of the closed-loop map
   // The gather plan (record offsets, data/constant/diagonal bits, output targets) depends on
   // the lane only (k == 0 differs in two constants) and is built once per factorisation;
-  // frag_load issues the 13 gathers unconditionally one stage ahead, frag_finish applies the
+  // frag_load issues the 8 gathers unconditionally two stages ahead, frag_finish applies the
   // selects when the stage is factorised, so no load is sunk into a lane-divergent branch.
+  static constexpr int NGATHER = 8;
   struct FragPlan {
-    int off[13];  // record offsets: data entries, or the record's constant slots (CONE, CZERO, SELP, SEL0)
+    int off[NGATHER];  // record offsets: data entries, or the record's constant slots (CONE, CZERO, SELP, SEL0)
     unsigned dlt;  // D registers on the diagonal of H (+ delta)
-    int st_a[4], st_p[4], lp1[4], lp2[4];  // per D register: record / LDS targets (discard slots if none)
+    int st_p[4], lp1[4], lp2[4];  // per D register: record / LDS targets (discard slots if none)
   };
+  // record slot of entry (i, j) of E^ (either stage class k = 0 / k > 0): its data word, or the
+  // constant slot holding its value; CZERO when !keep
+  static MR_HD int ehat_slot(int i, int j, bool keep) {
+    int idx;
+    bool data;
+    T cst;
+    if (!keep) return RCF::CZERO;
+    ehat_src(1, i, j, idx, data, cst);
+    if (data) return idx;
+    const bool one_pos = cst != T(0);
+    ehat_src(0, i, j, idx, data, cst);
+    const bool one_k0 = cst != T(0);
+    return one_pos ? (one_k0 ? RCF::CONE : RCF::SELP) : (one_k0 ? RCF::SEL0 : RCF::CZERO);
+  }
   static MR_HD void frag_plan(int lane, FragPlan& fp) {
     const int g = lane >> 4, c = lane & 15;
     fp.dlt = 0u;
-    // record slot of entry (i, j) of E^: its data word, or the constant slot holding its value
-    auto src = [&](int i, int j, bool keep) -> int {
-      int idx;
-      bool data;
-      T cst;
-      if (!keep) return RCF::CZERO;
-      ehat_src(1, i, j, idx, data, cst);
-      if (data) return idx;
-      const bool one_pos = cst != T(0);
-      ehat_src(0, i, j, idx, data, cst);
-      const bool one_k0 = cst != T(0);
-      return one_pos ? (one_k0 ? RCF::CONE : RCF::SELP) : (one_k0 ? RCF::SEL0 : RCF::CZERO);
-    };
 #pragma unroll
-    for (int s = 0; s < 4; ++s) fp.off[s] = src(4 * s + g, c, true);
-    fp.off[4] = src(c, NX + g, (c < NX) & (g < NU));
+    for (int s = 0; s < 4; ++s) fp.off[s] = ehat_slot(4 * s + g, c, true);
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const int a = drow(g, v);
       const int a_ = a < NZ ? a : 0;
-      fp.off[5 + v] = a < NZ ? (c < NZ ? RCF::H + hidx(a_, c) : (c == 14 ? RCF::G0 + a_ : RCF::G1 + a_)) : RCF::CZERO;
+      fp.off[4 + v] = a < NZ ? (c < NZ ? RCF::H + hidx(a_, c) : (c == 14 ? RCF::G0 + a_ : RCF::G1 + a_)) : RCF::CZERO;
       if (a < NZ && a == c) fp.dlt |= 1u << v;
-      fp.off[9 + v] = src(a, c, (a < NX) & ((c < NX) | (c == 14)));
-      // outputs of D register v: closed-loop map, packed-upper P | p0 | p1, LDS image of P^
+      // outputs of D register v: packed-upper P | p0 | p1, LDS image of P^
       const int junk_r = RCF::JUNK, junk_l = LJUNK_OFF - LP_OFF + lane;  // lp* index from LP
       const bool ax = a < NX, up = ax & (c < NX) & (a <= c);
       const bool c14 = ax & (c == 14), c15 = ax & (c == 15);
-      fp.st_a[v] = (ax & (c < NX)) ? RCF::ACL + a * NX + c : (c14 ? RCF::FF + a : junk_r);
       fp.st_p[v] = up ? RCF::P + pidx(a, c) : (c14 ? RCF::PV0 + a : (c15 ? RCF::PV1 + a : junk_r));
       fp.lp1[v] = up ? a * LDS_LD + c : (c14 ? a * LDS_LD + 11 : (c15 ? a * LDS_LD + 12 : junk_l));
       fp.lp2[v] = up ? c * LDS_LD + a : fp.lp1[v];
@@ -605,18 +602,14 @@ struct WaveSolver {
   }
   static MR_HD void frag_load(const WBuf<T>& rb, unsigned ro, const FragPlan& fp, T* raw) {
 #pragma unroll
-    for (int q = 0; q < 13; ++q) raw[q] = rb.ld(ro, (unsigned)fp.off[q]);
+    for (int q = 0; q < NGATHER; ++q) raw[q] = rb.ld(ro, (unsigned)fp.off[q]);
   }
   // operands straight from the gathered words (constants come from the record's constant slots)
-  static MR_HD void frag_finish(const T* dd, const T* raw, T* eb, T* hc, T& ab, T* ac) {
+  static MR_HD void frag_finish(const T* dd, const T* raw, T* eb, T* hc) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) eb[s] = raw[s];
-    ab = raw[4];
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      hc[v] = raw[5 + v] + dd[v];
-      ac[v] = raw[9 + v];
-    }
+    for (int v = 0; v < 4; ++v) hc[v] = raw[4 + v] + dd[v];
   }
 
   // ---------------- sweep 2: Riccati factorisation on the matrix cores ----------------
@@ -625,10 +618,12 @@ struct WaveSolver {
   //   Q    = (H + dI | g0 | g1) + E^T X   4 x v_mfma          (E^'s B fragment is E^T's A fragment)
   //   Q_uu = L L^T (3x3, wave-uniform),   W = L^{-1} Q_u.     (one column per lane)
   //   P^   = Q_x. - W^T W                 1 x v_mfma          (upper triangle mirrored)
-  //   K = -L^{-T} W_x,  k0 | k1 = -L^{-T} w0 | w1, and the closed-loop map for the forward pass
-  //   A + B K | B (k0 + mu k1) + c        1 x v_mfma
-  // Stage k-2's record is gathered (13 loads per lane) while stage k is factorised.
-  MR_SWEEP bool riccati(T delta, T mu) {
+  //   K = -L^{-T} W_x,  k0 | k1 = -L^{-T} w0 | w1
+  // Stage k-2's record is gathered (8 loads per lane) while stage k is factorised.  The record gets
+  // P, p0, p1, K, k0, k1 of stage k; the forward recursion forms A dx + B du + c from the stage's
+  // Jacobian itself (no closed-loop map is stored: 132 fewer words written per stage and
+  // factorisation, and a smaller record).
+  MR_SWEEP bool riccati(T delta, T /*mu*/) {
     MR_ASSUME_LDS_STATE();
     const int l = ln, N = wu(w, this->N), g = l >> 4, c = l & 15;
     const Wv w = this->w;
@@ -647,11 +642,10 @@ struct WaveSolver {
     // lane-constant 0/1 selectors: per-lane picks as products (exact for finite values), so the
     // step has no lane-divergent branches
     const T sg[3] = {g == 0 ? T(1) : T(0), g == 1 ? T(1) : T(0), g == 2 ? T(1) : T(0)};
-    const T sk = ((g < NU) & (c < NX)) ? T(-1) : T(0), sf = ((g < NU) & (c == 14)) ? T(-1) : T(0);
     // operand gathers run two stages ahead of the factorisation (three rotating buffers): a record
     // gather is an Infinity-Cache / HBM round trip (the 8 192 instances' records do not fit the L2),
     // longer than one stage's arithmetic
-    T raw_a[13], raw_b[13], raw_c[13];
+    T raw_a[NGATHER], raw_b[NGATHER], raw_c[NGATHER];
     frag_load(rb, R(N - 1), fp, raw_a);
     frag_load(rb, R(N >= 2 ? N - 2 : 0), fp, raw_b);
     {  // terminal cost-to-go: P_N = H_N,xx + delta I, p_N = g_N.  Branch-free (lanes >= NX write
@@ -681,8 +675,8 @@ struct WaveSolver {
     auto step = [&](int k, const T* raw_use, T* raw_fill) -> bool {
       // stage offsets as visibly wave-uniform values (SGPR soffsets, not per-lane waterfall loops)
       const unsigned Rk = (unsigned)wu(w, (int)R(k));
-      T eb[4], dq[4], dacl[4], ab;
-      frag_finish(dd, raw_use, eb, dq, ab, dacl);
+      T eb[4], dq[4];
+      frag_finish(dd, raw_use, eb, dq);
       frag_load(rb, (unsigned)wu(w, (int)R(k >= 2 ? k - 2 : 0)), fp, raw_fill);  // unconditional: k < 2 re-read stage 0's record
       // X = P^ E^  (A fragment s: P^[c][4s+g])
       // two independent 2-MFMA accumulation chains (k = 0..7 | 8..15) instead of one 4-long
@@ -738,15 +732,9 @@ struct WaveSolver {
           rb.st(kcol ? -kc[a] : (kf0 ? -k0[a] : -k1[a]), Rk, idx);
         }
       }
-      // closed-loop map (A + B K | B (k0 + mu k1) + c) for the forward recursion
-      const T kg = kc[0] * sg[0] + kc[1] * sg[1] + kc[2] * sg[2];
-      const T kf = (k0[0] + mu * k1[0]) * sg[0] + (k0[1] + mu * k1[1]) * sg[1] + (k0[2] + mu * k1[2]) * sg[2];
-      const T kb = kg * sk + kf * sf;  // -K[g][c] (c < 11), -(k0 + mu k1)[g] (c = 14), else 0
-      wmfma(w, ab, kb, dacl);
 #pragma unroll
       for (int v = 0; v < 4; ++v) {  // branch-free: lanes without a target write their discard slot
         const T pv = dq[v] - dw[v];
-        rb.st(dacl[v], Rk, (unsigned)fp.st_a[v]);
         rb.st(pv, Rk, (unsigned)fp.st_p[v]);
         LP[fp.lp1[v]] = pv;
         LP[fp.lp2[v]] = pv;
@@ -798,20 +786,24 @@ struct WaveSolver {
       auto R = [](int k) { return (unsigned)(SSF::NF * WL) + (unsigned)k * (unsigned)RC_STRIDE; };
       MR_LDS T* const LDX = lds + LDX_OFF;
       // One recursion step per stage k = 0..N with three lane groups sharing the same dot product
-      // row . dx_k (dx_k gathered from lanes 0..10): group 0 (lanes 0..10) row i of the closed-loop
-      // map -> dx_{k+1}[i]; group 1 (lanes 16..26) row i of P_k -> the costate step
+      // row . dx_k (dx_k gathered from lanes 0..10): group 0 (lanes 0..10) row i of [A | c] of the
+      // stage map E^ -> (A dx_k + c)[i]; group 1 (lanes 16..26) row i of P_k -> the costate step
       // dnu_k[i] = P_k dx_k + p_k - nu_k (k >= 1); group 2 (lanes 32..34) row a of K_k ->
-      // du_k[a] = K_k dx_k + k0 + mu k1.  Every lane gathers its row from stage k's record (one
+      // du_k[a] = K_k dx_k + k0 + mu k1.  Then group 0 adds B du_k (du_k read from group 2):
+      // dx_{k+1} = A dx_k + B du_k + c.  Every lane gathers its row from stage k's record (one
       // record, a few cache lines per load), instead of each lane reading its own stage's P and K
       // afterwards (a different cache line per lane and load).  Lanes without a row read the
-      // record's zero slot.
+      // record's zero slot; E^'s structural entries come from the record's constant slots.
       const int grp = ln >> 4, r = ln & 15;
       const bool g0r = (grp == 0) & (r < NX), g1r = (grp == 1) & (r < NX), g2r = (grp == 2) & (r < NU);
-      int roff[NX], c0off, c1off;
+      const int r0 = g0r ? r : 0;
+      int roff[NX], boff[NU], c0off, c1off;
 #pragma unroll
       for (int j = 0; j < NX; ++j)
-        roff[j] = g0r ? RCF::ACL + r * NX + j : (g1r ? RCF::P + pidx(r, j) : (g2r ? RCF::K + r * NX + j : RCF::CZERO));
-      c0off = g0r ? RCF::FF + r : (g1r ? RCF::PV0 + r : (g2r ? RCF::K0 + r : RCF::CZERO));
+        roff[j] = g0r ? ehat_slot(r0, j, true) : (g1r ? RCF::P + pidx(r, j) : (g2r ? RCF::K + r * NX + j : RCF::CZERO));
+#pragma unroll
+      for (int a = 0; a < NU; ++a) boff[a] = ehat_slot(r0, NX + a, g0r);
+      c0off = g0r ? ehat_slot(r0, 14, true) : (g1r ? RCF::PV0 + r : (g2r ? RCF::K0 + r : RCF::CZERO));
       c1off = g1r ? RCF::PV1 + r : (g2r ? RCF::K1 + r : RCF::CZERO);
       const unsigned nuoff = (unsigned)(SSF::NU + (g1r ? r : 0)) * WL;
       auto nu_ld = [&](int kk) -> T {
@@ -830,11 +822,12 @@ struct WaveSolver {
 #define MR_FWD_PD 4
 #endif
       constexpr int PD = MR_FWD_PD;  // prefetch distance (stages), register ring
-      T rw_r[PD][NX], c0_r[PD], c1_r[PD], nu_r[PD];
+      T rw_r[PD][NX], bw_r[PD][NU], c0_r[PD], c1_r[PD], nu_r[PD];
 #pragma unroll
       for (int d = 0; d < PD; ++d) {
         const int kk = d < N ? d : N;
         for (int j = 0; j < NX; ++j) rw_r[d][j] = wb.ld(R(kk), (unsigned)roff[j]);
+        for (int a = 0; a < NU; ++a) bw_r[d][a] = wb.ld(R(kk), (unsigned)boff[a]);
         c0_r[d] = wb.ld(R(kk), (unsigned)c0off);
         c1_r[d] = wb.ld(R(kk), (unsigned)c1off);
         nu_r[d] = nu_ld(kk);
@@ -844,11 +837,13 @@ struct WaveSolver {
         for (int d = 0; d < PD; ++d) {
           const int k = k0 + d;
           if (k > N) break;  // wave-uniform
-          T rw[NX];
+          T rw[NX], bw[NU];
           for (int j = 0; j < NX; ++j) rw[j] = rw_r[d][j];
+          for (int a = 0; a < NU; ++a) bw[a] = bw_r[d][a];
           const T c0 = c0_r[d], c1 = c1_r[d], nuv = nu_r[d];
           const int kn = k + PD < N ? k + PD : N;
           for (int j = 0; j < NX; ++j) rw_r[d][j] = wb.ld(R(kn), (unsigned)roff[j]);
+          for (int a = 0; a < NU; ++a) bw_r[d][a] = wb.ld(R(kn), (unsigned)boff[a]);
           c0_r[d] = wb.ld(R(kn), (unsigned)c0off);
           c1_r[d] = wb.ld(R(kn), (unsigned)c1off);
           nu_r[d] = nu_ld(kn);
@@ -869,8 +864,12 @@ struct WaveSolver {
           T acc = c0 + mu * c1;
           for (int j = 0; j < NX; ++j) acc += rw[j] * dxv[j];
 #endif
-          dxi = g0r ? acc : T(0);
-          lds[lbase + lstep * k] = acc;
+          // dx_{k+1} = (A dx_k + c) + B du_k on group 0, du_k from group 2 (lanes 32..34)
+          T accx = acc;
+#pragma unroll
+          for (int a = 0; a < NU; ++a) accx += bw[a] * wbcast(w, acc, 32 + a);
+          dxi = g0r ? accx : T(0);
+          lds[lbase + lstep * k] = g0r ? accx : acc;
           const bool dn = g1r & (k >= 1);
           if constexpr (SSL) {
             if (dn) ss[(SSF::DNU + r) * WL + k] = acc - nuv;
@@ -957,6 +956,7 @@ struct WaveSolver {
     const T s_phi = T(2.3), delta_sw = T(1), eta = T(1e-4), g_th = T(1e-5), g_ph = T(1e-5);
     const int nb = 1 - cur;
     const int k = ln;
+    const int N = wu(w, this->N);  // wave-uniform: the SOC re-roll's lane index must be an SGPR
     T z[NZS], dz[NZS], s_c[NI], ds[NI];
     load_z(cur, z);
     for (int i = 0; i < NZS; ++i) dz[i] = own() ? S(SSF::DZ + i) : T(0);

@@ -142,7 +142,9 @@ def test_c3_full_batch_lane_rows():
     s = solver_for_config("C3", 8192)
     o = _np(s.solve(b))
     ok = o["status"] == 0
-    assert ok.mean() >= 0.8, np.bincount(o["status"], minlength=5)
+    # ~94 % solve; the unsolved ones are unsolved by the oracle's IPM and by SLSQP too
+    # (profiles/r02_audit_C3.json)
+    assert ok.mean() >= 0.9, np.bincount(o["status"], minlength=5)
     _check_feasible(cfg, o, ok, 1e-6)
     m = b["max_error"][ok]
     assert (np.abs(o["eC"][1:, ok]) <= m + 1e-6).all()  # |e_C(S_i, X_i)| <= max_error, i >= 1
