@@ -57,6 +57,8 @@ def main():
            "longest": [{"i": int(i), "iters": int(it[i]), "status": int(status[i]), "start_ms": float(st[i]),
                         "dur_ms": float(dur[i])} for i in long_[:8]],
            "longest_solo_ms": solo,
+           "last_to_end": [{"i": int(i), "iters": int(it[i]), "status": int(status[i]), "start_ms": float(st[i]),
+                            "end_ms": float(en[i])} for i in np.argsort(-en)[:8]],
            "end_of_bulk_ms_p99": float(np.quantile(en, 0.99)), "end_p999": float(np.quantile(en, 0.999))}
     os.makedirs("gpurun_out", exist_ok=True)
     np.savez_compressed(f"gpurun_out/timeline_{name}_d{order}.npz", start=st, end=en, iters=it, status=status)
