@@ -80,9 +80,9 @@ typedef struct mr_config {
   double m, Iz, lf, lr, Cf, Cr, T_max, r_wheel, C_wheel, R, rho, C_d, A_f, C_roll, g, max_steer_deg,
       Vblendmin, Vblendmax;
   /* workgroup dispatch order of a batch (results do not depend on it: instances are independent):
-     0 = instance order; 1 = (default) the instances whose initial speed is near the ends of the
-     range (<= 16.5 or >= 39 m/s: through the 15 m/s blend corner / the hardest contouring cases, the
-     ones that run hundreds of iterations) first, so the batch's longest solves start early */
+     0 = instance order; 1 = (default) a stable three-tier partition so the likely long solves start
+     first: tier 0 = v >= 40 m/s, or throttle <= -0.5 at v <= 20 m/s (hard braking through a blend
+     corner of the model); tier 1 = the rest outside 16.5 < v < 39; tier 2 = the others */
   int32_t dispatch_order;
 } mr_config;
 
