@@ -29,9 +29,35 @@ MR_HD double mr_log(double a) { return log(a); }
 MR_HD double mr_abs(double a) { return fabs(a); }
 MR_HD float mr_sin(float a) { return sinf(a); }
 MR_HD float mr_cos(float a) { return cosf(a); }
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(MR_LIBM_F32)
+// fp32 on the device, for the model's steering and slip angles (|a| < 1.6 rad): tan from the hardware
+// sine / cosine (the library tanf carries a ~140-instruction large-argument reduction), atan2 by an
+// odd degree-15 polynomial on [0, 1] with octant reduction (max error 1.3e-7 rad, ~2 ulp, vs ~45
+// instructions with a division for the library's).  fp64 and the host build keep libm.
+MR_HD float mr_tan(float a) { return __sinf(a) * __builtin_amdgcn_rcpf(__cosf(a)); }
+MR_HD float mr_atan2(float y, float x) {
+  const float ax = fabsf(x), ay = fabsf(y);
+  const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+  const float q = mx > 0.0f ? mn * __builtin_amdgcn_rcpf(mx) : 0.0f;
+  const float s = q * q;
+  float p = -0.004073309246450663f;
+  p = p * s + 0.021946610882878304f;
+  p = p * s - 0.056063175201416016f;
+  p = p * s + 0.09656256437301636f;
+  p = p * s - 0.13915802538394928f;
+  p = p * s + 0.19948509335517883f;
+  p = p * s - 0.3333010673522949f;
+  p = p * s + 0.999999463558197f;
+  float r = q * p;
+  r = ay > ax ? 1.5707963267948966f - r : r;
+  r = x < 0.0f ? 3.141592653589793f - r : r;
+  return copysignf(r, y);
+}
+#else
 MR_HD float mr_tan(float a) { return tanf(a); }
-MR_HD float mr_atan(float a) { return atanf(a); }
 MR_HD float mr_atan2(float y, float x) { return atan2f(y, x); }
+#endif
+MR_HD float mr_atan(float a) { return atanf(a); }
 MR_HD float mr_sqrt(float a) { return sqrtf(a); }
 MR_HD float mr_exp(float a) { return expf(a); }
 MR_HD float mr_log(float a) { return logf(a); }
