@@ -818,65 +818,67 @@ struct WaveSolver {
       const int lstep = g0r ? 12 : (g2r ? 3 : 0);
       T dxi = T(0);
       if (ln < NX) LDX[ln] = T(0);
-#ifndef MR_FWD_PD
-#define MR_FWD_PD 4
-#endif
-      constexpr int PD = MR_FWD_PD;  // prefetch distance (stages), register ring
-      T rw_r[PD][NX], bw_r[PD][NU], c0_r[PD], c1_r[PD], nu_r[PD];
+      // Row gathers run two stages ahead in three rotating register sets, the loop unrolled by three
+      // with one exit test per step at its end (uniform control, no copies of in-flight loads): the
+      // waits for a set are exact vmcnt counts, not drains at the loop head.
+      struct FwdRow {
+        T rw[NX], bw[NU], c0, c1, nu;
+      };
+      auto fload = [&](int kk, FwdRow& f) {
+        kk = kk < N ? kk : N;
+        const unsigned ro = (unsigned)wu(w, (int)R(kk));
 #pragma unroll
-      for (int d = 0; d < PD; ++d) {
-        const int kk = d < N ? d : N;
-        for (int j = 0; j < NX; ++j) rw_r[d][j] = wb.ld(R(kk), (unsigned)roff[j]);
-        for (int a = 0; a < NU; ++a) bw_r[d][a] = wb.ld(R(kk), (unsigned)boff[a]);
-        c0_r[d] = wb.ld(R(kk), (unsigned)c0off);
-        c1_r[d] = wb.ld(R(kk), (unsigned)c1off);
-        nu_r[d] = nu_ld(kk);
-      }
-      for (int k0 = 0; k0 <= N; k0 += PD) {
+        for (int j = 0; j < NX; ++j) f.rw[j] = wb.ld(ro, (unsigned)roff[j]);
 #pragma unroll
-        for (int d = 0; d < PD; ++d) {
-          const int k = k0 + d;
-          if (k > N) break;  // wave-uniform
-          T rw[NX], bw[NU];
-          for (int j = 0; j < NX; ++j) rw[j] = rw_r[d][j];
-          for (int a = 0; a < NU; ++a) bw[a] = bw_r[d][a];
-          const T c0 = c0_r[d], c1 = c1_r[d], nuv = nu_r[d];
-          const int kn = k + PD < N ? k + PD : N;
-          for (int j = 0; j < NX; ++j) rw_r[d][j] = wb.ld(R(kn), (unsigned)roff[j]);
-          for (int a = 0; a < NU; ++a) bw_r[d][a] = wb.ld(R(kn), (unsigned)boff[a]);
-          c0_r[d] = wb.ld(R(kn), (unsigned)c0off);
-          c1_r[d] = wb.ld(R(kn), (unsigned)c1off);
-          nu_r[d] = nu_ld(kn);
-          T dxv[NX];
-          wgather<T, NX>(w, dxi, dxv);
+        for (int a = 0; a < NU; ++a) f.bw[a] = wb.ld(ro, (unsigned)boff[a]);
+        f.c0 = wb.ld(ro, (unsigned)c0off);
+        f.c1 = wb.ld(ro, (unsigned)c1off);
+        f.nu = nu_ld(wu(w, kk));
+      };
+      auto fstep = [&](int k, const FwdRow& f) {
+        T dxv[NX];
+        wgather<T, NX>(w, dxi, dxv);
 #if MR_FWD_TREE
-          // the 11-term dot as three interleaved chains (critical path 4 FMAs + 2 adds, not 11)
-          T a0 = c0 + mu * c1, a1 = rw[1] * dxv[1], a2 = rw[2] * dxv[2];
-          a0 += rw[0] * dxv[0];
+        // the 11-term dot as three interleaved chains (critical path 4 FMAs + 2 adds, not 11)
+        T a0 = f.c0 + mu * f.c1, a1 = f.rw[1] * dxv[1], a2 = f.rw[2] * dxv[2];
+        a0 += f.rw[0] * dxv[0];
 #pragma unroll
-          for (int j = 3; j < NX; j += 3) {
-            a0 += rw[j] * dxv[j];
-            if (j + 1 < NX) a1 += rw[j + 1] * dxv[j + 1];
-            if (j + 2 < NX) a2 += rw[j + 2] * dxv[j + 2];
-          }
-          const T acc = (a0 + a1) + a2;
-#else
-          T acc = c0 + mu * c1;
-          for (int j = 0; j < NX; ++j) acc += rw[j] * dxv[j];
-#endif
-          // dx_{k+1} = (A dx_k + c) + B du_k on group 0, du_k from group 2 (lanes 32..34)
-          T accx = acc;
-#pragma unroll
-          for (int a = 0; a < NU; ++a) accx += bw[a] * wbcast(w, acc, 32 + a);
-          dxi = g0r ? accx : T(0);
-          lds[lbase + lstep * k] = g0r ? accx : acc;
-          const bool dn = g1r & (k >= 1);
-          if constexpr (SSL) {
-            if (dn) ss[(SSF::DNU + r) * WL + k] = acc - nuv;
-          } else {  // branch-free: other lanes write stage k's record discard slot
-            wb.st(acc - nuv, (unsigned)k, dn ? (unsigned)(SSF::DNU + r) * WL : R(k) + RCF::JUNK - (unsigned)k);
-          }
+        for (int j = 3; j < NX; j += 3) {
+          a0 += f.rw[j] * dxv[j];
+          if (j + 1 < NX) a1 += f.rw[j + 1] * dxv[j + 1];
+          if (j + 2 < NX) a2 += f.rw[j + 2] * dxv[j + 2];
         }
+        const T acc = (a0 + a1) + a2;
+#else
+        T acc = f.c0 + mu * f.c1;
+        for (int j = 0; j < NX; ++j) acc += f.rw[j] * dxv[j];
+#endif
+        // dx_{k+1} = (A dx_k + c) + B du_k on group 0, du_k from group 2 (lanes 32..34)
+        T accx = acc;
+#pragma unroll
+        for (int a = 0; a < NU; ++a) accx += f.bw[a] * wbcast(w, acc, 32 + a);
+        dxi = g0r ? accx : T(0);
+        lds[lbase + lstep * k] = g0r ? accx : acc;
+        const bool dn = g1r & (k >= 1);
+        if constexpr (SSL) {
+          if (dn) ss[(SSF::DNU + r) * WL + k] = acc - f.nu;
+        } else {  // branch-free: other lanes write stage k's record discard slot
+          wb.st(acc - f.nu, (unsigned)k, dn ? (unsigned)(SSF::DNU + r) * WL : R(k) + RCF::JUNK - (unsigned)k);
+        }
+      };
+      FwdRow fa, fb, fc;
+      fload(0, fa);
+      fload(1, fb);
+      for (int k = 0;; k += 3) {
+        fload(k + 2, fc);
+        fstep(k, fa);
+        if (k == N) break;
+        fload(k + 3, fa);
+        fstep(k + 1, fb);
+        if (k + 1 == N) break;
+        fload(k + 4, fb);
+        fstep(k + 2, fc);
+        if (k + 2 == N) break;
       }
       wsync_lds(w);
       if (ln <= N)
