@@ -745,21 +745,17 @@ struct WaveSolver {
     // Pivots are tested once per three stages, at the loop latch: a failed stage only costs the
     // next two, and the loop keeps one back-edge block (exact prefetch waits at the loop head).
     // Buffer roles rotate a -> c -> b -> a over the three unrolled steps.
+    bool ok = true;
     for (int k = N - 1;; k -= 3) {
-      bool ok = step(k, raw_a, raw_c);
-      if (k == 0) {
-        if (!wuni(w, ok)) return false;
-        break;
-      }
+      ok = step(k, raw_a, raw_c) & ok;
+      if (k == 0) break;
       ok = step(k - 1, raw_b, raw_a) & ok;
-      if (k == 1) {
-        if (!wuni(w, ok)) return false;
-        break;
-      }
+      if (k == 1) break;
       ok = step(k - 2, raw_c, raw_b) & ok;
-      if (!wuni(w, ok)) return false;
       if (k == 2) break;
+      if (!wuni(w, ok)) return false;
     }
+    if (!wuni(w, ok)) return false;
     wsync(w);  // records (P, K, closed-loop map) visible to every lane
     return true;
   }
