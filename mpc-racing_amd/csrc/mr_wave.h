@@ -386,7 +386,10 @@ struct WaveSolver {
     const unsigned long long te0 = trace ? MR_CLOCK() : 0ull;
 #endif
     if (own()) {
-      MR_GLOBAL T* Rk = R(k);
+      // the stage record through a buffer resource: its stores do not order this sweep's later
+      // stage-field loads (different memory objects to the compiler), so those issue early
+      const WBuf<T> rbe(rc, (unsigned)WL * (unsigned)RC_STRIDE);
+      const unsigned Rk = (unsigned)k * (unsigned)RC_STRIDE;
       T H[NH], g0[NZ], g1[NZ], gl[NZ], st[NZ];
       for (int i = 0; i < NH; ++i) H[i] = T(0);
       for (int i = 0; i < NZ; ++i) { g0[i] = g1[i] = gl[i] = st[i] = T(0); }
@@ -405,11 +408,11 @@ struct WaveSolver {
         c[9] = (k == 0 ? z[11] : z[9]) - znext[9];
         c[10] = (k == 0 ? z[12] : z[10]) - znext[10];
         for (int i = 0; i < NX; ++i) {
-          Rk[RCF::C + i] = c[i];
+          rbe.st(c[i], 0u, Rk + RCF::C + i);
           pr_l = mr_max(pr_l, mr_abs(c[i]));
           th_l += mr_abs(c[i]);
         }
-        for (int i = 0; i < 48; ++i) Rk[RCF::J + i] = J[i];
+        for (int i = 0; i < 48; ++i) rbe.st(J[i], 0u, Rk + RCF::J + i);
         T at[NX], bt[NU];
         apply_At(J, k, nun, at);
         apply_Bt(J, k, nun, bt);
@@ -500,8 +503,8 @@ struct WaveSolver {
         for (int i = 0; i < NX; ++i) st_l = mr_max(st_l, mr_abs(st[i]));
       if (k < N)
         for (int i = NX; i < NZ; ++i) st_l = mr_max(st_l, mr_abs(st[i]));
-      for (int i = 0; i < NH; ++i) Rk[RCF::H + i] = H[i];
-      for (int i = 0; i < NZ; ++i) { Rk[RCF::G0 + i] = g0[i]; Rk[RCF::G1 + i] = g1[i]; }
+      for (int i = 0; i < NH; ++i) rbe.st(H[i], 0u, Rk + RCF::H + i);
+      for (int i = 0; i < NZ; ++i) { rbe.st(g0[i], 0u, Rk + RCF::G0 + i); rbe.st(g1[i], 0u, Rk + RCF::G1 + i); }
     }
 #if MR_PHASE_CYCLES
     const unsigned long long te1 = trace ? MR_CLOCK() : 0ull;
