@@ -32,6 +32,11 @@
 extern "C" {
 #endif
 
+/* ABI version (mr_version()): bumped whenever a struct layout or an entry point's meaning changes, so
+   a caller built against another header can refuse to run (101: mr_config.dispatch_order,
+   mr_outputs.lam_g / timeline, status 4 = restoration failed) */
+#define MR_ABI_VERSION 101
+
 #define MR_OK 0
 #define MR_ERR_ARG (-1)
 #define MR_ERR_HIP (-2)
@@ -132,7 +137,9 @@ int mr_config_default(mr_config* cfg);
 int mr_create(mr_handle** h, const mr_config* cfg);
 int mr_destroy(mr_handle* h);
 /* Pacejka coefficients a[0..8] and vertical load Fz for the front and back tyre
-   (state dict keys front_tire.a / front_tire.Fz / back_tire.a / back_tire.Fz). */
+   (state dict keys front_tire.a / front_tire.Fz / back_tire.a / back_tire.Fz).  Synchronises the
+   handle's device before it replaces the constants the kernels read (solves in flight on any stream
+   finish first). */
 int mr_set_tyres(mr_handle* h, const double* a_front, double Fz_front, const double* a_back, double Fz_back);
 int mr_solve_batch(mr_handle* h, int32_t B, const mr_inputs* in, mr_outputs* out, void* hip_stream);
 /* Diagnostics: the handle's vehicle dynamics (fp64) at n points, device arrays x [n][6], u [n][2],
@@ -222,7 +229,8 @@ int mr_agent_sense(const mr_track* tr, int32_t n, const double* X, const double*
                    double lookback, double lookahead, double err_offset, double* progress, double* error, double* cx,
                    double* cy, double* max_error, void* hip_stream);
 /* One plant step per vehicle: state [6][n] = (x, y, yaw, v_x, v_y, yaw_dot), cmd [2][n] = (throttle - brake,
-   steer) -> out [6][n] (may alias state).  Model.step(throttle_cmd, steer_cmd, dt) of the models/ package. */
+   steer) -> out [6][n] (may alias state).  Model.step(throttle_cmd, steer_cmd, dt) of the models/ package.
+   Runs on the device that owns `state` (MR_ERR_ARG if it is not a HIP device pointer). */
 int mr_plant_step(int32_t model, int32_t n, const double* state, const double* cmd, double dt, double* out,
                   void* hip_stream);
 

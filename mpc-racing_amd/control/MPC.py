@@ -122,7 +122,13 @@ class MPC:
         lam = out["lam_g"][:, 0]
         if status in (0, 1):
             self.sol = info
-            self.dual = lam[~np.isnan(lam)]  # state0 rows absent when its throttle / steer is None
+            # the two state0 rate rows (the last two) exist only when state0 has a throttle / steer
+            # (MPC.py:145-149); any other row is kept in place, NaN or not, so the vector stays in
+            # opti.lam_g's row order
+            keep = np.ones(lam.shape[0], dtype=bool)
+            keep[-2] = state0.throttle is not None
+            keep[-1] = state0.steer is not None
+            self.dual = lam[keep]
         else:
             print(f"MPC solve did not converge: {info.status} after {info.iterations} iterations")
             self.sol = None

@@ -38,18 +38,33 @@ static int fail(int code, const std::string& msg) {
 }
 
 // Entry points switch to the handle's device for their HIP calls and restore the caller's current
-// device on return (a library call must not change it).
+// device on return (a library call must not change it).  A device that cannot be made current is an
+// error of the entry point (MR_GUARD_DEVICE), never a silent launch on whatever device is current.
 struct DeviceGuard {
   int prev = -1;
+  hipError_t err = hipSuccess;
   explicit DeviceGuard(int dev) {
     if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-    if (prev != dev) (void)hipSetDevice(dev);
+    if (prev != dev) err = hipSetDevice(dev);
   }
   ~DeviceGuard() {
     int cur = -1;
     if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
   }
 };
+#define MR_GUARD_DEVICE(dev)                                                                       \
+  DeviceGuard dg_(dev);                                                                            \
+  if (dg_.err != hipSuccess)                                                                       \
+    return fail(MR_ERR_HIP, std::string("hipSetDevice(") + std::to_string(dev) + "): " + hipGetErrorString(dg_.err))
+
+// The device that owns a device pointer (entry points without a handle: mr_plant_step).
+static int pointer_device(const void* p, int* dev) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) return -1;
+  if (a.type != hipMemoryTypeDevice && a.type != hipMemoryTypeManaged) return -1;
+  *dev = a.device;
+  return 0;
+}
 
 #define HIP_TRY(x)                                                                  \
   do {                                                                              \
@@ -381,12 +396,12 @@ __global__ __launch_bounds__(kTrackBlock) void mr_plant_step_kernel(int model, i
 
 extern "C" {
 
-int mr_version(void) { return 100; }
+int mr_version(void) { return MR_ABI_VERSION; }
 
 int mr_eval_dynamics(mr_handle* h, int32_t n, const double* x, const double* u, const double* nu, double* f,
                      double* J, double* H, void* hip_stream) {
   if (!h || !x || !u || !f || n < 0 || (J && (!H || !nu))) return fail(MR_ERR_ARG, "null argument");
-  DeviceGuard dg_(h->cfg.device);
+  MR_GUARD_DEVICE(h->cfg.device);
   ProbParams<double> P;
   fill_params<double>(h->cfg, h->tf, h->tr, P);
   hipStream_t st = (hipStream_t)hip_stream;
@@ -418,7 +433,14 @@ int mr_create(mr_handle** out, const mr_config* cfg) {
   if (cfg->precision != MR_PREC_FP64 && cfg->precision != MR_PREC_FP32) return fail(MR_ERR_ARG, "bad precision");
   if (cfg->max_batch < 1) return fail(MR_ERR_ARG, "max_batch < 1");
   if (!(cfg->Ts > 0)) return fail(MR_ERR_ARG, "Ts must be > 0");
-  DeviceGuard dg_(cfg->device);
+  {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+    if (cfg->device < 0 || cfg->device >= ndev)
+      return fail(MR_ERR_ARG, "device " + std::to_string(cfg->device) + " out of range (" + std::to_string(ndev) +
+                                  " HIP devices)");
+  }
+  MR_GUARD_DEVICE(cfg->device);
   mr_handle* h = new mr_handle();
   h->cfg = *cfg;
   h->have_tyres = 0;
@@ -460,7 +482,10 @@ int mr_set_tyres(mr_handle* h, const double* a_front, double Fz_front, const dou
   h->tf = pacejka_coef(a_front, Fz_front);
   h->tr = pacejka_coef(a_back, Fz_back);
   h->have_tyres = 1;
-  DeviceGuard dg_(h->cfg.device);
+  MR_GUARD_DEVICE(h->cfg.device);
+  // the kernels read the constants from this buffer while they run: a solve still in flight on any
+  // stream of the device (torch side streams do not order with the copy below) must finish first
+  HIP_TRY(hipDeviceSynchronize());
   return upload_params(h);
 }
 
@@ -479,7 +504,7 @@ int mr_solve_batch(mr_handle* h, int32_t B, const mr_inputs* in, mr_outputs* out
   const int m = h->cfg.model;
   if ((m == MR_MODEL_BLENDED_PACEJKA || m == MR_MODEL_DYNAMIC_PACEJKA) && !h->have_tyres)
     return fail(MR_ERR_STATE, "Pacejka model needs mr_set_tyres");
-  DeviceGuard dg_(h->cfg.device);
+  MR_GUARD_DEVICE(h->cfg.device);
   hipStream_t st = (hipStream_t)hip_stream;
   if (h->cfg.precision == MR_PREC_FP64) return dispatch_model<double>(h, B, in, out, st);
   return dispatch_model<float>(h, B, in, out, st);
@@ -496,7 +521,14 @@ int mr_track_create(mr_track** out, int32_t device, const double* t, int32_t n_t
   const TrackLayout Lay = track_layout(n_t, n_rows);
   std::vector<double> blob(Lay.total);
   track_tables(t, n_t, cx, cy, n_c, err_left, err_right, n_rows, blob.data());
-  DeviceGuard dg_(device);
+  {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+    if (device < 0 || device >= ndev)
+      return fail(MR_ERR_ARG, "device " + std::to_string(device) + " out of range (" + std::to_string(ndev) +
+                                  " HIP devices)");
+  }
+  MR_GUARD_DEVICE(device);
   mr_track* tr = new mr_track();
   tr->device = device;
   tr->nt = n_t;
@@ -526,7 +558,7 @@ int mr_track_destroy(mr_track* tr) {
     if (!tr) return fail(MR_ERR_ARG, "null track");                                              \
     if (n < 0) return fail(MR_ERR_ARG, "n < 0");                                                 \
     if (n == 0) return MR_OK;                                                                    \
-    DeviceGuard dg_(tr->device);                                                           \
+    MR_GUARD_DEVICE(tr->device);                                                                 \
     hipLaunchKernelGGL(kernel, dim3((n + kTrackBlock - 1) / kTrackBlock), dim3(kTrackBlock), 0,  \
                        (hipStream_t)hip_stream, tr->view, n, __VA_ARGS__);                       \
     HIP_TRY(hipGetLastError());                                                                  \
@@ -598,7 +630,7 @@ int mr_track_lane_table(const mr_track* centerline, const mr_track* lane, int32_
   if (centerline->device != lane->device) return fail(MR_ERR_ARG, "centerline and lane on different devices");
   if (n < 0) return fail(MR_ERR_ARG, "n < 0");
   if (n == 0) return MR_OK;
-  DeviceGuard dg_(centerline->device);
+  MR_GUARD_DEVICE(centerline->device);
   hipLaunchKernelGGL(mr_lane_table_kernel, dim3((n + kLaneWaves - 1) / kLaneWaves), dim3(64 * kLaneWaves), 0,
                      (hipStream_t)hip_stream, centerline->view, lane->view, (int)n, s, dist, s_lane);
   HIP_TRY(hipGetLastError());
@@ -611,6 +643,9 @@ int mr_plant_step(int32_t model, int32_t n, const double* state, const double* c
   if (model < MR_PLANT_KINEMATIC || model > MR_PLANT_BLENDED) return fail(MR_ERR_ARG, "unknown plant model");
   if (n < 0) return fail(MR_ERR_ARG, "n < 0");
   if (n == 0) return MR_OK;
+  int dev = -1;
+  if (pointer_device(state, &dev) != 0) return fail(MR_ERR_ARG, "state is not a HIP device pointer");
+  MR_GUARD_DEVICE(dev);  // the arrays' device, not whichever device is current
   hipLaunchKernelGGL(mr_plant_step_kernel, dim3((n + kTrackBlock - 1) / kTrackBlock), dim3(kTrackBlock), 0,
                      (hipStream_t)hip_stream, (int)model, (int)n, state, cmd, dt, out);
   HIP_TRY(hipGetLastError());

@@ -333,6 +333,16 @@ struct WaveSolver {
       Rk[RCF::CZERO] = T(0);
       Rk[RCF::SELP] = k > 0 ? T(1) : T(0);
       Rk[RCF::SEL0] = k > 0 ? T(0) : T(1);
+      if (k == N) {
+        // stage N has no dynamics and no gains: the evaluation and Riccati sweeps never write its
+        // Jacobian / defect / K / k0 / k1 slots, yet the forward recursion's last step (k = N) gathers
+        // them in its lane groups 0 and 2 (whose results go only to the unused LDX row N + 1 and
+        // du_N); zeros keep that step on defined values
+        for (int q = 0; q < 48; ++q) Rk[RCF::J + q] = T(0);
+        for (int q = 0; q < NX; ++q) Rk[RCF::C + q] = T(0);
+        for (int q = 0; q < NU * NX; ++q) Rk[RCF::K + q] = T(0);
+        for (int q = 0; q < NU; ++q) { Rk[RCF::K0 + q] = T(0); Rk[RCF::K1 + q] = T(0); }
+      }
     }
     gmax = wmax(w, gmax);
     th = wsum(w, th);
@@ -759,14 +769,15 @@ struct WaveSolver {
       if (!wuni(w, ok)) return false;
     }
     if (!wuni(w, ok)) return false;
-    wsync(w);  // records (P, K, closed-loop map) visible to every lane
+    wsync(w);  // records (P, p, K, k0, k1) visible to every lane
     return true;
   }
 
   // ---------------- sweep 3: forward substitution, slack/dual steps ----------------
-  //   dx_{k+1} = (A + B K)_k dx_k + f_k with the closed-loop map of the Riccati sweep: lane
-  //   i < 11 owns dx[i], the 11 values are shared with v_readlane, one 11-term dot per step.
-  //   Then stage-parallel: du_k = K_k dx_k + k0 + mu k1, slack/dual steps, costates.
+  //   Sequential part: per stage, three lane groups share one 11-term dot with dx_k (gathered from
+  //   lanes 0..10): [A | c] rows -> A dx_k + c, P_k rows -> the costate step, K_k rows -> du_k =
+  //   K_k dx_k + k0 + mu k1; then dx_{k+1} = A dx_k + c + B du_k (stage Jacobian from the record,
+  //   no closed-loop map).  Then stage-parallel: slack / multiplier steps and the step limits.
   MR_SWEEP void forward(T& ap, T& ad, T& gphi) {
     MR_UNIFORM_P();
     MR_ASSUME_LDS_STATE();

@@ -7,6 +7,7 @@ CSRC = os.path.abspath(os.path.join(HERE, "..", "csrc"))
 PRODUCT_LIB = os.path.join(CSRC, "libmpcracing.so")
 HOST_TWIN_LIB = os.path.join(CSRC, "libmpcracing_host.so")
 
+ABI_VERSION = 101  # MR_ABI_VERSION of include/mpcracing.h
 MR_MODEL = {"kin": 0, "dyn": 1, "blend": 2, "blend_pacejka": 3, "dyn_pacejka": 4}
 MR_PREC = {"fp64": 0, "fp32": 1}
 STATUS = {0: "solved", 1: "acceptable", 2: "max_iter", 3: "failed", 4: "lane_infeasible"}
@@ -87,7 +88,11 @@ def load_product(path=None):
     if _product is None:
         if not os.path.exists(path):
             raise RuntimeError(f"libmpcracing.so not built ({path}); run `python __graft_entry__.py build`")
-        _product = _bind_product(ctypes.CDLL(path))
+        lib = _bind_product(ctypes.CDLL(path))
+        if lib.mr_version() != ABI_VERSION:
+            raise RuntimeError(f"{path}: ABI version {lib.mr_version()}, this binding expects {ABI_VERSION} "
+                               "(rebuild with `python __graft_entry__.py build`)")
+        _product = lib
     return _product
 
 

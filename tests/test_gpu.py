@@ -227,6 +227,25 @@ def test_abi_errors():
         s.solve(wl.make_batch("C2", limit=4))  # B > max_batch
     with pytest.raises(RuntimeError):
         BatchSolver(20, "blend_pacejka", max_batch=1).solve(wl.make_batch("C2", limit=1))  # no tyres set
+    # a device index the machine does not have is an error of mr_create / mr_track_create, not a silent
+    # handle on whichever device is current
+    ndev = torch.cuda.device_count()
+    with pytest.raises(RuntimeError, match="out of range"):
+        BatchSolver(20, "kin", max_batch=1, device=ndev)
+    import ctypes
+    from mpcracing import abi
+    lib = abi.load_product()
+    tr = ctypes.c_void_p()
+    t = np.zeros(12)
+    t[4:] = np.arange(1, 9)
+    cx = np.ascontiguousarray(np.arange(8, dtype=np.float64))
+    P = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))  # noqa: E731
+    assert lib.mr_track_create(ctypes.byref(tr), ndev, P(t), 12, P(cx), P(cx), 8, 8.0, None, None, 0) == -1
+    assert b"out of range" in lib.mr_last_error()
+    # mr_plant_step runs on the device that owns its arrays; a host pointer is rejected
+    st = np.zeros((6, 4))
+    assert lib.mr_plant_step(0, 4, st.ctypes.data_as(ctypes.c_void_p), st.ctypes.data_as(ctypes.c_void_p), 0.05,
+                             st.ctypes.data_as(ctypes.c_void_p), None) == -1
 
 
 @pytest.mark.parametrize("model", ["kin", "dyn", "blend", "blend_pacejka", "dyn_pacejka"])
