@@ -61,9 +61,11 @@ extern "C" {
 #define MR_STATUS_SOLVED 0
 #define MR_STATUS_ACCEPTABLE 1
 #define MR_STATUS_MAX_ITER 2
-#define MR_STATUS_FAILED 3 /* non-finite values or no inertia-correct factorisation */
-#define MR_STATUS_LANE_INFEASIBLE 4 /* converged, but a lane row needed its elastic slack (> 1e-6 m):
-                                       the hard-constrained NLP is locally infeasible */
+#define MR_STATUS_FAILED 3 /* non-finite values, no inertia-correct factorisation, or the restoration
+                              phase's line search failed (IPOPT: Restoration_Failed) */
+#define MR_STATUS_INFEASIBLE 4 /* the restoration phase converged to a minimiser of the constraint
+                                  violation the original problem does not accept (IPOPT:
+                                  Infeasible_Problem_Detected, "local infeasibility") */
 
 typedef struct mr_config {
   int32_t N;           /* horizon (FixedControllerParameters.N = 30 unless the caller passes N) */

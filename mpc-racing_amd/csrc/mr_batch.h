@@ -70,6 +70,9 @@ MR_HD SolveOut solve_instance(const ProbParams<T>& P, const mr_inputs& in, const
   I.n = (int)in.runtime[3 * B + i];
   if (I.n < 1) I.n = 1;
   I.beta = T(in.runtime[4 * B + i]);
+  I.org[0] = T(X0);
+  I.org[1] = T(Y0);
+  I.org[2] = T(s0);
   Solver<T, MODEL> S(P, I, W);
   if (out.trace && out.trace_instance == i) { S.trace = out.trace; S.trace_cap = out.trace_cap; }
   S.init(in.u_init ? in.u_init + i : nullptr, B);
@@ -92,7 +95,6 @@ MR_HD SolveOut solve_instance(const ProbParams<T>& P, const mr_inputs& in, const
       out.eL[k * B + i] = (double)e.eL;
     }
   }
-  if (P.lane && (r.status == 0 || r.status == 1) && (double)S.lane_violation() > 1e-6) r.status = MR_STATUS_LANE_INFEASIBLE;
   out.status[i] = r.status;
   out.iters[i] = r.iters;
   if (out.obj) out.obj[i] = r.obj - (double)P.lambda_s * s0;  // -lambda_s * S_N in global s

@@ -45,7 +45,17 @@ struct WF {
     Z0 = 0, Z1 = Z0 + NZS, DZ = Z1 + NZS, S0 = DZ + NZS, S1 = S0 + NI, LAM = S1 + NI, DLAM = LAM + NI,
     DS = DLAM + NI, NUv = DS + NI, DNU = NUv + NX, H = DNU + NX, G0 = H + NH, G1 = G0 + NZ, GL = G1 + NZ,
     J = GL + NZ, C = J + 48, P = C + NX, PV0 = P + NP, PV1 = PV0 + NX, K = PV1 + NX, K0 = K + NU * NX,
-    K1 = K0 + NU, NF = K1 + NU
+    K1 = K0 + NU,
+    // watchdog snapshot: the iterate and the search direction where the watchdog started
+    WZ = K1 + NU, WSL = WZ + NZS, WLAM = WSL + NI, WNU = WLAM + NI, WDZ = WNU + NX, WDS = WDZ + NZS,
+    WDLAM = WDS + NI, WDNU = WDLAM + NI,
+    // restoration phase: row relaxations p, n, their bound duals and steps, the reference point z_R
+    RP = WDNU + NX, RN = RP + NI, RVP = RN + NI, RVN = RVP + NI, RDP = RVN + NI, RDN = RDP + NI, RDVP = RDN + NI,
+    RDVN = RDVP + NI, RY = RDVN + NI, RDY = RY + NI, RZ = RDY + NI,
+    // restoration relaxations of the 6 vehicle dynamics rows of x_{k+1} = F(x_k, u_k) (stage k < N):
+    // p, n, duals, steps, and the condensed disturbance weight / gradient for the Riccati sweep
+    CP = RZ + NZS, CN = CP + 6, CVP = CN + 6, CVN = CVP + 6, CDP = CVN + 6, CDN = CDP + 6, CDVP = CDN + 6,
+    CDVN = CDVP + 6, CSW = CDVN + 6, CGW0 = CSW + 6, CGW1 = CGW0 + 6, NF = CGW1 + 6
   };
 };
 
@@ -81,6 +91,7 @@ struct Inst {
   T ax[5], ay[5];  // ascending coefficients in sigma = s - s0, minus the (X0, Y0) origin
   T max_err, alpha_c, d_max, q_vy, beta;
   int n;
+  T org[3];  // global X0, Y0, s0 of the solver origin (the restoration phase's proximity scaling)
 };
 
 template <typename T>
@@ -262,6 +273,10 @@ MR_HD void make_row(const ProbParams<T>& P, const Inst<T>& I, int k, int r, cons
 //   and the same KKT point as the hard row whenever that NLP is feasible and lane_pen > |lambda*|).
 template <typename T>
 MR_HD bool lane_active(const ProbParams<T>& P, int k) { return P.lane && k >= 1; }
+// lane_pen > 0: the elastic form below; otherwise the hard rows e_C + m >= 0, m - e_C >= 0 of the
+// reference (t fixed at 0, row JL + 2 inactive), whose infeasible starts the restoration phase handles
+template <typename T>
+MR_HD bool lane_elastic(const ProbParams<T>& P) { (void)P; return false; }
 
 template <typename T>
 MR_HD void lane_d(const Inst<T>& I, T eC, T t, T* d) {
@@ -337,6 +352,26 @@ MR_HD void faug(const ProbParams<T>& P, int k, const T* z, T* xn) {
   xn[8] = z[12];
   xn[9] = (k == 0) ? z[11] : z[9];
   xn[10] = (k == 0) ? z[12] : z[10];
+}
+
+// Restoration objective's proximity term (zeta/2) sum D_i^2 (z_i - zR_i)^2 over the reference's own
+// variables (MPC.py:62-64): States X_i and S_hat_i (stage indices 0..6, k >= 1; X_0, S_0 are fixed) and
+// U (indices 11, 12, k < N); D_i = min(1, 1/|zR_i|) of the global value.  Adds gradient / diagonal
+// Hessian (either may be null), returns the term.
+template <typename T>
+MR_HD T prox_term(const Inst<T>& I, int k, int N, const T* z, const T* zr, T zeta, T* g, T* H) {
+  T v = T(0);
+  for (int i = 0; i < NZ; ++i) {
+    const bool on = (i <= 6 && k >= 1) || ((i == 11 || i == 12) && k < N);
+    if (!on) continue;
+    const T glob = zr[i] + (i == 0 ? I.org[0] : (i == 1 ? I.org[1] : (i == 6 ? I.org[2] : T(0))));
+    const T D = mr_min(T(1), T(1) / mr_max(mr_abs(glob), T(1e-30)));
+    const T w = zeta * D * D, dz = z[i] - zr[i];
+    v += T(0.5) * w * dz * dz;
+    if (g) g[i] += w * dz;
+    if (H) H[hidx(i, i)] += w;
+  }
+  return v;
 }
 
 // ----------------------------------------------------------------------------------------
@@ -423,6 +458,155 @@ MR_HD void apply_Bt(const T* J, int k, const T* v, T* y) {
 }
 
 // ----------------------------------------------------------------------------------------
+// One-sided inequality rows in the Newton system (regular and restoration phase)
+// ----------------------------------------------------------------------------------------
+// A row d(z) >= 0 is d(z) - s = 0 with the slack s >= 0 (bound dual lam, the row multiplier).  In the
+// restoration phase (IPOPT's l1 restoration NLP, Waechter & Biegler 2006 sec. 3.3) it is relaxed to
+// d(z) - s - p + n = 0 with p, n >= 0 (bound duals vp, vn) and cost rho (p + n).  The slack-like
+// variables are condensed out of the Newton system: the row adds sig a a^T to the Hessian and
+// a (c0 + mu c1) to the gradient (a = grad d):
+//   regular:      sig = lam / s,                          c0 = sig (d - s),  c1 = -1 / s
+//   restoration:  1 / sig = s / lam + p / vp + n / vn,    r = d - s - p + n,
+//                 c0 = sig (r - rho (n / vn - p / vp)),   c1 = -sig (1 / lam + 1 / vp - 1 / vn)
+template <typename T>
+MR_HD void row_cond(T d, T s, T lam, T& sig, T& c0, T& c1) {
+  sig = lam / s;
+  c0 = sig * (d - s);
+  c1 = -T(1) / s;
+}
+template <typename T>
+MR_HD void row_cond_r(T d, T s, T lam, T p, T n, T vp, T vn, T rho, T& sig, T& c0, T& c1) {
+  const T is = s / lam, ip = p / vp, in = n / vn;
+  sig = T(1) / (is + ip + in);
+  c0 = sig * ((d - s - p + n) - rho * (in - ip));
+  c1 = -sig * (T(1) / lam + T(1) / vp - T(1) / vn);
+}
+// Restoration row steps from the linearised residual e = (d - s - p + n) + a.dz: the new row
+// multiplier eta = sig (G - e), G = rho (n/vn - p/vp) + mu (1/lam + 1/vp - 1/vn), then
+//   ds = (mu/s - eta) s/lam,  dp = (mu/p - rho - eta) p/vp,  dn = (mu/n - rho + eta) n/vn,
+//   dlam = eta - lam,  dvp = rho + eta - vp,  dvn = rho - eta - vn   (primal-dual bound-dual steps)
+template <typename T>
+MR_HD void row_steps_r(T e, T s, T lam, T p, T n, T vp, T vn, T rho, T mu, T& ds, T& dp, T& dn, T& dlam, T& dvp,
+                       T& dvn) {
+  const T is = s / lam, ip = p / vp, in = n / vn;
+  const T sig = T(1) / (is + ip + in);
+  const T G = rho * (in - ip) + mu * (T(1) / lam + T(1) / vp - T(1) / vn);
+  const T eta = sig * (G - e);
+  ds = (mu / s - eta) * is;
+  dp = (mu / p - rho - eta) * ip;
+  dn = (mu / n - rho + eta) * in;
+  dlam = eta - lam;
+  dvp = rho + eta - vp;
+  dvn = rho - eta - vn;
+}
+// IPOPT's closed-form start of the restoration variables for a row residual c = d - s (so that
+// c - p + n = 0): n = b + sqrt(b^2 + mu c / (2 rho)), b = (mu - rho c) / (2 rho), p = c + n; written
+// without cancellation for b < 0
+template <typename T>
+MR_HD void resto_pn(T c, T mu, T rho, T& p, T& n) {
+  const T b = (mu - rho * c) / (T(2) * rho), q = mu * c / (T(2) * rho);
+  const T r = mr_sqrt(b * b + q);
+  n = b >= T(0) ? b + r : q / (r - b);
+  p = c + n;
+}
+// Restoration phase, relaxed vehicle dynamics rows F_i(x_k, u_k) - x_{k+1,i} - p_i + n_i = 0 (i < 6):
+// the relaxation enters x_{k+1} as a disturbance w = dn - dp with cost 1/2 sw w^2 + (gw0 + mu gw1) w
+// (p, n condensed as in row_cond_r: 1/sw = p/vp + n/vn, gw0 = sw rho (n/vn - p/vp),
+// gw1 = sw (1/vp - 1/vn)).  Minimising the cost-to-go of stage k+1, V(xi) = 1/2 xi^T P xi +
+// (p0 + mu p1)^T xi, over w gives the cost-to-go of xi = y + E w as a function of y:
+//   M = P_vv + diag(sw) = L L^T,  Y = L^-1 P_v.,  P~ = P - Y^T Y,  p~ = p - Y^T L^-1 (p_v + gw)
+// (false if M is not positive definite: the stage's inertia is wrong, as for a failed Q_uu pivot).
+template <typename T>
+MR_HD bool chol6(const T* M, T* L) {  // M, L: 6x6 row-major, L lower
+  for (int i = 0; i < 6; ++i)
+    for (int j = 0; j <= i; ++j) {
+      T v = M[i * 6 + j];
+      for (int q = 0; q < j; ++q) v -= L[i * 6 + q] * L[j * 6 + q];
+      if (i == j) {
+        if (!(v > T(0))) return false;
+        L[i * 6 + i] = mr_sqrt(v);
+      } else {
+        L[i * 6 + j] = v / L[j * 6 + j];
+      }
+    }
+  return true;
+}
+template <typename T>
+MR_HD void lsolve6(const T* L, T* b) {
+  for (int i = 0; i < 6; ++i) {
+    T v = b[i];
+    for (int q = 0; q < i; ++q) v -= L[i * 6 + q] * b[q];
+    b[i] = v / L[i * 6 + i];
+  }
+}
+template <typename T>
+MR_HD void ltsolve6(const T* L, T* b) {
+  for (int i = 5; i >= 0; --i) {
+    T v = b[i];
+    for (int q = i + 1; q < 6; ++q) v -= L[q * 6 + i] * b[q];
+    b[i] = v / L[i * 6 + i];
+  }
+}
+template <typename T>
+MR_HD bool noise_cond(T* Pm, T* p0, T* p1, const T* sw, const T* gw0, const T* gw1) {
+  T M[36], L[36];
+  for (int i = 0; i < 6; ++i)
+    for (int j = 0; j < 6; ++j) M[i * 6 + j] = Pm[pidx(i, j)] + (i == j ? sw[i] : T(0));
+  if (!chol6(M, L)) return false;
+  T Y[6][NX], y0[6], y1[6];
+  for (int j = 0; j < NX; ++j) {
+    T col[6];
+    for (int i = 0; i < 6; ++i) col[i] = Pm[pidx(i, j)];
+    lsolve6(L, col);
+    for (int i = 0; i < 6; ++i) Y[i][j] = col[i];
+  }
+  for (int i = 0; i < 6; ++i) { y0[i] = p0[i] + gw0[i]; y1[i] = p1[i] + gw1[i]; }
+  lsolve6(L, y0);
+  lsolve6(L, y1);
+  for (int i = 0; i < NX; ++i) {
+    for (int j = i; j < NX; ++j) {
+      T v = Pm[pidx(i, j)];
+      for (int a = 0; a < 6; ++a) v -= Y[a][i] * Y[a][j];
+      Pm[pidx(i, j)] = v;
+    }
+  }
+  for (int i = 0; i < NX; ++i) {
+    T v0 = p0[i], v1 = p1[i];
+    for (int a = 0; a < 6; ++a) { v0 -= Y[a][i] * y0[a]; v1 -= Y[a][i] * y1[a]; }
+    p0[i] = v0;
+    p1[i] = v1;
+  }
+  return true;
+}
+// the disturbance step w = -M^-1 (nu_y[0..5] + gw), nu_y = P y + p the cost-to-go gradient at y
+template <typename T>
+MR_HD void noise_step(const T* Pm, const T* sw, const T* rhs, T* w) {
+  T M[36], L[36];
+  for (int i = 0; i < 6; ++i)
+    for (int j = 0; j < 6; ++j) M[i * 6 + j] = Pm[pidx(i, j)] + (i == j ? sw[i] : T(0));
+  chol6(M, L);
+  for (int i = 0; i < 6; ++i) w[i] = -rhs[i];
+  lsolve6(L, w);
+  ltsolve6(L, w);
+}
+// the relaxation steps of one dynamics row from its disturbance step w (eta = sw (w + G)):
+//   dp = (-eta - rho + mu/p) p/vp,  dn = (eta - rho + mu/n) n/vn,  dvp = rho + eta - vp,  dvn = rho - eta - vn
+template <typename T>
+MR_HD void dyn_steps_r(T w, T p, T n, T vp, T vn, T rho, T mu, T& dp, T& dn, T& dvp, T& dvn) {
+  const T ip = p / vp, in = n / vn;
+  const T sw = T(1) / (ip + in);
+  const T G = rho * (in - ip) + mu * (T(1) / vp - T(1) / vn);
+  const T eta = sw * (w + G);
+  dp = (-eta - rho + mu / p) * ip;
+  dn = (eta - rho + mu / n) * in;
+  dvp = rho + eta - vp;
+  dvn = rho - eta - vn;
+}
+// restoration-phase constants (IPOPT resto_penalty_parameter, required_infeasibility_reduction,
+// bound_mult_reset_threshold)
+constexpr double RESTO_RHO = 1000.0, RESTO_KAPPA = 0.9, RESTO_MULT_RESET = 1000.0;
+
+// ----------------------------------------------------------------------------------------
 // The solver
 // ----------------------------------------------------------------------------------------
 struct SolveOut {
@@ -442,6 +626,12 @@ struct SolveOut {
 #ifndef MR_LS_FAIL_MAX
 #define MR_LS_FAIL_MAX 1000000
 #endif
+#ifndef MR_WD_TRIGGER
+#define MR_WD_TRIGGER 10  // IPOPT watchdog_shortened_iter_trigger (0: watchdog off)
+#endif
+#ifndef MR_WD_TRIAL_MAX
+#define MR_WD_TRIAL_MAX 3  // IPOPT watchdog_trial_iter_max
+#endif
 constexpr int FMAX = MR_FMAX;
 
 template <typename T, int MODEL>
@@ -460,6 +650,13 @@ struct Solver {
   // iteration aggregates (eval sweep)
   T stat_max, pr_max, theta, slam_max, slam_min, nu1, lam1, fval, logs;
   int me, mi;
+  // restoration phase: mode, its penalty and proximity weight, and the original problem's state
+  bool resto = false;
+  T rho = T(RESTO_RHO), zeta = T(0);
+  T mu_o, th_entry, delta_last_o, theta_max_o, theta_min_o;
+  T ofilt_th[FMAX], ofilt_ph[FMAX];
+  int onfilt;
+  T tho_acc, pho_acc;  // original theta / barrier objective of the last trial point (restoration)
   double* trace = nullptr;  // optional per-iteration record (diagnostics)
   int trace_cap = 0;
 
@@ -487,7 +684,8 @@ struct Solver {
       d[2 * r + 1] = rows[r].hi - rows[r].c;
     }
     const int la = lane_active(P, k) ? 1 : 0;
-    act[JL] = act[JL + 1] = act[JL + 2] = la;
+    act[JL] = act[JL + 1] = la;
+    act[JL + 2] = la && lane_elastic(P);
     lane_d(I, e.eC, z[14], d + JL);
   }
 
@@ -511,7 +709,7 @@ struct Solver {
       }
       Err<T> e;
       errors(I, z[0], z[1], z[6], e, false);
-      z[14] = lane_active(P, k) ? mr_max(mr_abs(e.eC) - I.max_err, T(0)) + T(1e-2) : T(0);
+      z[14] = lane_active(P, k) && lane_elastic(P) ? mr_max(mr_abs(e.eC) - I.max_err, T(0)) + T(1e-2) : T(0);
       store_z(k, 0, z);
 #ifdef MR_DEBUG_PRINT
       if (trace) printf("init k=%d vx=%g readback=%g X=%g S=%g\n", k, (double)z[3], (double)W(k, WF::Z0 + 3),
@@ -582,6 +780,7 @@ struct Solver {
   // Applies the lazy dual update of the previous accepted step first.
   MR_HD void eval_sweep(T mu_prev) {
     const T kappa_sigma = T(1e10);
+    zeta = mr_sqrt(mu_prev);  // restoration proximity weight (IPOPT: resto_proximity_weight sqrt(mu))
     stat_max = pr_max = theta = T(0);
     slam_max = T(0);
     slam_min = T(1e30);
@@ -626,6 +825,30 @@ struct Solver {
         c[8] = z[12] - znext[8];
         c[9] = (k == 0 ? z[11] : z[9]) - znext[9];
         c[10] = (k == 0 ? z[12] : z[10]) - znext[10];
+        if (resto) {  // relaxed vehicle rows F - x' - p + n (the S / previous-control rows are definitions)
+          const T kappa_sigma = T(1e10);
+          for (int i = 0; i < 6; ++i) {
+            const T p = W(k, WF::CP + i), n = W(k, WF::CN + i);
+            T vp = W(k, WF::CVP + i) + alpha_d * W(k, WF::CDVP + i);
+            T vn = W(k, WF::CVN + i) + alpha_d * W(k, WF::CDVN + i);
+            vp = mr_min(mr_max(vp, mu_prev / (kappa_sigma * p)), kappa_sigma * mu_prev / p);
+            vn = mr_min(mr_max(vn, mu_prev / (kappa_sigma * n)), kappa_sigma * mu_prev / n);
+            W(k, WF::CVP + i) = vp;
+            W(k, WF::CVN + i) = vn;
+            c[i] += n - p;
+            const T ip = p / vp, in = n / vn, sw = T(1) / (ip + in);
+            W(k, WF::CSW + i) = sw;
+            W(k, WF::CGW0 + i) = sw * rho * (in - ip);
+            W(k, WF::CGW1 + i) = sw * (T(1) / vp - T(1) / vn);
+            slam_max = mr_max(slam_max, mr_max(p * vp, n * vn));
+            slam_min = mr_min(slam_min, mr_min(p * vp, n * vn));
+            lam1 += mr_abs(vp) + mr_abs(vn);
+            logs += mr_log(p) + mr_log(n);
+            mi += 2;
+            fval += rho * (p + n);
+            stat_max = mr_max(stat_max, mr_max(mr_abs(rho - nun[i] - vp), mr_abs(rho + nun[i] - vn)));
+          }
+        }
         for (int i = 0; i < NX; ++i) {
           W(k, WF::C + i) = c[i];
           pr_max = mr_max(pr_max, mr_abs(c[i]));
@@ -639,10 +862,16 @@ struct Solver {
         for (int i = 0; i < NX; ++i) st[i] += at[i];
         for (int i = 0; i < NU; ++i) st[NX + i] += bt[i];
       }
-      // cost
+      // cost: the scaled objective, or the restoration phase's proximity term
       Err<T> e;
       errors(I, z[0], z[1], z[6], e, true);
-      fval += stage_cost(P, I, k, z, e, sc, gl, H);
+      if (resto) {
+        T zr[NZS];
+        for (int i = 0; i < NZS; ++i) zr[i] = W(k, WF::RZ + i);
+        fval += prox_term(I, k, N, z, zr, zeta, gl, H);
+      } else {
+        fval += stage_cost(P, I, k, z, e, sc, gl, H);
+      }
       for (int i = 0; i < NZ; ++i) { g0[i] += gl[i]; st[i] += gl[i]; }
       // -nu_k on the state part (k >= 1)
       if (k >= 1) for (int i = 0; i < NX; ++i) st[i] -= nuk[i];
@@ -651,24 +880,52 @@ struct Solver {
       int act[NI];
       Row<T> rows[NROW];
       row_values(k, z, e, d, act, rows);
-      T lam_j[NI], s_j[NI];
+      T lam_j[NI], sig_j[NI], c0_j[NI], c1_j[NI], y_j[NI];  // y: the row multiplier in W and grad L
+      auto clip = [&](T v, T x) { return mr_min(mr_max(v, mu_prev / (kappa_sigma * x)), kappa_sigma * mu_prev / x); };
       for (int j = 0; j < NI; ++j) {
+        lam_j[j] = sig_j[j] = c0_j[j] = c1_j[j] = y_j[j] = T(0);
         if (!act[j]) continue;
         T s = W(k, sf(cur) + j);
-        T lam = W(k, WF::LAM + j) + alpha_d * W(k, WF::DLAM + j);
-        lam = mr_min(mr_max(lam, mu_prev / (kappa_sigma * s)), kappa_sigma * mu_prev / s);
+        T lam = clip(W(k, WF::LAM + j) + alpha_d * W(k, WF::DLAM + j), s);
         W(k, WF::LAM + j) = lam;
         lam_j[j] = lam;
-        s_j[j] = s;
+        y_j[j] = lam;  // regular phase: the slack's bound dual is the row multiplier
         T rd = d[j] - s;
-        pr_max = mr_max(pr_max, mr_abs(rd));
-        theta += mr_abs(rd);
         T sl = s * lam;
         slam_max = mr_max(slam_max, sl);
         slam_min = mr_min(slam_min, sl);
         lam1 += mr_abs(lam);
         logs += mr_log(s);
         mi += 1;
+        if (resto) {
+          const T p = W(k, WF::RP + j), n = W(k, WF::RN + j);
+          const T vp = clip(W(k, WF::RVP + j) + alpha_d * W(k, WF::RDVP + j), p);
+          const T vn = clip(W(k, WF::RVN + j) + alpha_d * W(k, WF::RDVN + j), n);
+          W(k, WF::RVP + j) = vp;
+          W(k, WF::RVN + j) = vn;
+          // restoration: the row's equality multiplier y is its own variable (IPOPT's y_d, started at 0,
+          // stepped with the primal step size), tied to the slack's bound dual only through stationarity
+          const T y = W(k, WF::RY + j) + alpha_p * W(k, WF::RDY + j);
+          W(k, WF::RY + j) = y;
+          y_j[j] = y;
+#ifndef MR_RESTO_YSTAT
+#define MR_RESTO_YSTAT 1
+#endif
+          if (MR_RESTO_YSTAT) stat_max = mr_max(stat_max, mr_abs(y - lam));
+          rd = rd - p + n;
+          slam_max = mr_max(slam_max, mr_max(p * vp, n * vn));
+          slam_min = mr_min(slam_min, mr_min(p * vp, n * vn));
+          lam1 += mr_abs(vp) + mr_abs(vn);
+          logs += mr_log(p) + mr_log(n);
+          mi += 2;
+          fval += rho * (p + n);
+          stat_max = mr_max(stat_max, mr_max(mr_abs(rho + y - vp), mr_abs(rho - y - vn)));
+          row_cond_r(d[j], s, lam, p, n, vp, vn, rho, sig_j[j], c0_j[j], c1_j[j]);
+        } else {
+          row_cond(d[j], s, lam, sig_j[j], c0_j[j], c1_j[j]);
+        }
+        pr_max = mr_max(pr_max, mr_abs(rd));
+        theta += mr_abs(rd);
       }
       for (int r = 0; r < NROW; ++r) {
         const Row<T>& R = rows[r];
@@ -676,12 +933,11 @@ struct Solver {
         T sig_sum = T(0), gsc0 = T(0), gsc1 = T(0), lamdiff = T(0);
         for (int sd = 0; sd < 2; ++sd) {
           int j = 2 * r + sd;
-          T sig = lam_j[j] / s_j[j];
           T sgn = sd == 0 ? T(1) : T(-1);
-          sig_sum += sig;
-          gsc0 += sgn * sig * (d[j] - s_j[j]);
-          gsc1 += -sgn / s_j[j];
-          lamdiff += sgn * lam_j[j];
+          sig_sum += sig_j[j];
+          gsc0 += sgn * c0_j[j];
+          gsc1 += sgn * c1_j[j];
+          lamdiff += sgn * y_j[j];
         }
         for (int a = 0; a < R.n; ++a) {
           g0[R.idx[a]] += R.a[a] * gsc0;
@@ -691,27 +947,19 @@ struct Solver {
         }
       }
       if (lane_active(P, k)) {
-        // rows e_C + m + t (slot JL) and m - e_C + t (JL+1) in z; t condensed out
+        // hard lane rows e_C + m >= 0 (slot JL) and m - e_C >= 0 (JL+1), nonlinear in (X, Y, S)
         const int id3[3] = {0, 1, 6};
-        T s0 = s_j[JL], s1 = s_j[JL + 1];
-        T sig0 = lam_j[JL] / s0, sig1 = lam_j[JL + 1] / s1;
-        T lamdiff = lam_j[JL] - lam_j[JL + 1];
-        T gz0 = sig0 * (d[JL] - s0) - sig1 * (d[JL + 1] - s1);
-        T gz1 = -T(1) / s0 + T(1) / s1;
-        T htt, hd, gt0, gt1;
-        lane_block(k, cur, d, htt, hd, gt0, gt1);
+        const T sig_sum = sig_j[JL] + sig_j[JL + 1];
+        const T gz0 = c0_j[JL] - c0_j[JL + 1], gz1 = c1_j[JL] - c1_j[JL + 1];
+        const T lamdiff = y_j[JL] - y_j[JL + 1];
         int q = 0;
         for (int a = 0; a < 3; ++a) {
-          g0[id3[a]] += e.gC[a] * (gz0 - hd * gt0 / htt);
-          g1[id3[a]] += e.gC[a] * (gz1 - hd * gt1 / htt);
+          g0[id3[a]] += e.gC[a] * gz0;
+          g1[id3[a]] += e.gC[a] * gz1;
           st[id3[a]] -= lamdiff * e.gC[a];
-          for (int bb = a; bb < 3; ++bb, ++q) {
-            H[hidx(id3[a], id3[bb])] += (sig0 + sig1 - hd * hd / htt) * e.gC[a] * e.gC[bb] - lamdiff * e.hC[q];
-          }
+          for (int bb = a; bb < 3; ++bb, ++q)
+            H[hidx(id3[a], id3[bb])] += sig_sum * e.gC[a] * e.gC[bb] - lamdiff * e.hC[q];
         }
-        fval += sc * P.lane_pen * z[14];
-        T stt = sc * P.lane_pen - lam_j[JL] - lam_j[JL + 1] - lam_j[JL + 2];
-        stat_max = mr_max(stat_max, mr_abs(stt));
       }
       // stationarity: x-part for k >= 1, u-part for k < N
       if (k >= 1) for (int i = 0; i < NX; ++i) stat_max = mr_max(stat_max, mr_abs(st[i]));
@@ -750,6 +998,11 @@ struct Solver {
       T J[48], c[NX];
       for (int i = 0; i < 48; ++i) J[i] = W(k, WF::J + i);
       for (int i = 0; i < NX; ++i) c[i] = W(k, WF::C + i);
+      if (resto) {  // the relaxed vehicle rows of x_{k+1} = F(x_k, u_k): minimise over the disturbance
+        T sw[6], gw0[6], gw1[6];
+        for (int i = 0; i < 6; ++i) { sw[i] = W(k, WF::CSW + i); gw0[i] = W(k, WF::CGW0 + i); gw1[i] = W(k, WF::CGW1 + i); }
+        if (!noise_cond(Pm, p0, p1, sw, gw0, gw1)) return false;
+      }
       // PA (11x11) column by column and PB (11x3)
       T PA[NX][NX], PB[NX][NU];
       for (int j = 0; j < NX; ++j) {
@@ -893,22 +1146,34 @@ struct Solver {
       }
       dz[14] = T(0);
       if (lane_active(P, k)) {
-        T htt, hd, gt0, gt1;
-        lane_block(k, cur, d, htt, hd, gt0, gt1);
-        T gdz = e.gC[0] * dz[0] + e.gC[1] * dz[1] + e.gC[2] * dz[6];
-        T dt = -(hd * gdz + gt0 + mu * gt1) / htt;
-        dz[14] = dt;
-        adz[JL] = gdz + dt;
-        adz[JL + 1] = -gdz + dt;
-        adz[JL + 2] = dt;
-        gphi += sc * P.lane_pen * dt;
+        const T gdz = e.gC[0] * dz[0] + e.gC[1] * dz[1] + e.gC[2] * dz[6];
+        adz[JL] = gdz;
+        adz[JL + 1] = -gdz;
+        adz[JL + 2] = T(0);
       }
       for (int i = 0; i < NZS; ++i) W(k, WF::DZ + i) = dz[i];
       for (int j = 0; j < NI; ++j) {
         if (!act[j]) continue;
         T s = W(k, sf(cur) + j), lam = W(k, WF::LAM + j);
-        T ds = adz[j] + (d[j] - s);
-        T dl = mu / s - lam - (lam / s) * ds;
+        T ds, dl;
+        if (resto) {
+          const T p = W(k, WF::RP + j), n = W(k, WF::RN + j), vp = W(k, WF::RVP + j), vn = W(k, WF::RVN + j);
+          T dp, dn, dvp, dvn;
+          row_steps_r(adz[j] + (d[j] - s - p + n), s, lam, p, n, vp, vn, rho, mu, ds, dp, dn, dl, dvp, dvn);
+          W(k, WF::RDP + j) = dp;
+          W(k, WF::RDN + j) = dn;
+          W(k, WF::RDVP + j) = dvp;
+          W(k, WF::RDVN + j) = dvn;
+          W(k, WF::RDY + j) = lam + dl - W(k, WF::RY + j);  // eta - y
+          gphi += (rho - mu / p) * dp + (rho - mu / n) * dn;
+          if (dp < T(0)) ap = mr_min(ap, -tau * p / dp);
+          if (dn < T(0)) ap = mr_min(ap, -tau * n / dn);
+          if (dvp < T(0)) ad = mr_min(ad, -tau * vp / dvp);
+          if (dvn < T(0)) ad = mr_min(ad, -tau * vn / dvn);
+        } else {
+          ds = adz[j] + (d[j] - s);
+          dl = mu / s - lam - (lam / s) * ds;
+        }
         W(k, WF::DS + j) = ds;
         W(k, WF::DLAM + j) = dl;
         gphi -= mu * ds / s;
@@ -921,6 +1186,32 @@ struct Solver {
         apply_A(J, k, dx, t);
         apply_B(J, k, dz + NX, tb);
         for (int i = 0; i < NX; ++i) dx[i] = t[i] + tb[i] + W(k, WF::C + i);
+        if (resto) {  // + the disturbance of the relaxed vehicle rows, w = -M^-1 (nu_y + gw)
+          T Pn[NP], sw[6], rhs[6], w[6];
+          for (int i = 0; i < NP; ++i) Pn[i] = W(k + 1, WF::P + i);
+          for (int i = 0; i < 6; ++i) {
+            T v = W(k + 1, WF::PV0 + i) + mu * W(k + 1, WF::PV1 + i);
+            for (int l = 0; l < NX; ++l) v += Pn[pidx(i, l)] * dx[l];
+            rhs[i] = v + W(k, WF::CGW0 + i) + mu * W(k, WF::CGW1 + i);
+            sw[i] = W(k, WF::CSW + i);
+          }
+          noise_step(Pn, sw, rhs, w);
+          for (int i = 0; i < 6; ++i) {
+            dx[i] += w[i];
+            const T p = W(k, WF::CP + i), n = W(k, WF::CN + i), vp = W(k, WF::CVP + i), vn = W(k, WF::CVN + i);
+            T dp, dn, dvp, dvn;
+            dyn_steps_r(w[i], p, n, vp, vn, rho, mu, dp, dn, dvp, dvn);
+            W(k, WF::CDP + i) = dp;
+            W(k, WF::CDN + i) = dn;
+            W(k, WF::CDVP + i) = dvp;
+            W(k, WF::CDVN + i) = dvn;
+            gphi += (rho - mu / p) * dp + (rho - mu / n) * dn;
+            if (dp < T(0)) ap = mr_min(ap, -tau * p / dp);
+            if (dn < T(0)) ap = mr_min(ap, -tau * n / dn);
+            if (dvp < T(0)) ad = mr_min(ad, -tau * vp / dvp);
+            if (dvn < T(0)) ad = mr_min(ad, -tau * vn / dvn);
+          }
+        }
         // costate nu_{k+1} = P_{k+1} dx_{k+1} + p_{k+1}
         for (int i = 0; i < NX; ++i) {
           T v = W(k + 1, WF::PV0 + i) + mu * W(k + 1, WF::PV1 + i);
@@ -936,7 +1227,7 @@ struct Solver {
   MR_HD bool trial(T alpha, bool soc, T& th_t, T& ph_t) {
     const int nb = 1 - cur;
     th_t = T(0);
-    T fv = T(0), lg = T(0);
+    T fv = T(0), lg = T(0), lgr = T(0), tho = T(0), fo = T(0);  // lgr, tho, fo: restoration phase only
     T z[NZS], zt[NZS], zpl[NZS], zroll[NX];
     bool ok = true;
     for (int k = 0; k <= N; ++k) {
@@ -961,17 +1252,33 @@ struct Solver {
         Row<T> rowsp[NROW];
         row_values(k, zpl, ep, dp, actp, rowsp);
       }
+      T dyn = T(0);  // this stage's share of theta not from rows (the dynamics defect)
       for (int j = 0; j < NI; ++j) {
         if (!act[j]) continue;
         T st = W(k, sf(cur) + j) + alpha * W(k, WF::DS + j);
         if (soc) st += d[j] - dp[j];
         if (!(st > T(0))) ok = false;
         W(k, sf(nb) + j) = st;
-        th_t += mr_abs(d[j] - st);
         lg += mr_log(st > T(0) ? st : T(1));
+        if (resto) {
+          const T pt = W(k, WF::RP + j) + alpha * W(k, WF::RDP + j), nt = W(k, WF::RN + j) + alpha * W(k, WF::RDN + j);
+          if (!(pt > T(0)) || !(nt > T(0))) ok = false;
+          th_t += mr_abs(d[j] - st - pt + nt);
+          tho += mr_abs(d[j] - st);
+          lgr += mr_log(pt > T(0) ? pt : T(1)) + mr_log(nt > T(0) ? nt : T(1));
+          fv += rho * (pt + nt);
+        } else {
+          th_t += mr_abs(d[j] - st);
+        }
       }
-      fv += stage_cost(P, I, k, zt, e, sc, (T*)nullptr, (T*)nullptr);
-      if (lane_active(P, k)) fv += sc * P.lane_pen * zt[14];
+      if (resto) {
+        T zr[NZS];
+        for (int i = 0; i < NZS; ++i) zr[i] = W(k, WF::RZ + i);
+        fv += prox_term(I, k, N, zt, zr, zeta, (T*)nullptr, (T*)nullptr);
+        fo += stage_cost(P, I, k, zt, e, sc, (T*)nullptr, (T*)nullptr);
+      } else {
+        fv += stage_cost(P, I, k, zt, e, sc, (T*)nullptr, (T*)nullptr);
+      }
       if (k < N) {
         T xn[NX];
         faug<T, MODEL>(P, k, zt, xn);
@@ -980,13 +1287,29 @@ struct Solver {
         } else {
           for (int i = 0; i < NX; ++i) {
             T xt = W(k + 1, zf(cur) + i) + alpha * W(k + 1, WF::DZ + i);
-            th_t += mr_abs(xn[i] - xt);
+            T rel = T(0);
+            if (resto && i < 6) {  // the relaxed vehicle rows
+              const T pt = W(k, WF::CP + i) + alpha * W(k, WF::CDP + i), nt = W(k, WF::CN + i) + alpha * W(k, WF::CDN + i);
+              if (!(pt > T(0)) || !(nt > T(0))) ok = false;
+              rel = nt - pt;
+              lgr += mr_log(pt > T(0) ? pt : T(1)) + mr_log(nt > T(0) ? nt : T(1));
+              fv += rho * (pt + nt);
+              tho += mr_abs(xn[i] - xt);
+            }
+            dyn += mr_abs(xn[i] - xt + rel);
+            if (resto && i >= 6) tho += mr_abs(xn[i] - xt);
           }
         }
       }
+      th_t += dyn;
+      if (!resto) tho += dyn;
       store_z(k, nb, zt);
     }
-    ph_t = fv - mu * lg;
+    ph_t = fv - mu * (lg + lgr);
+    if (resto) {  // the point measured as the original problem sees it (restoration exit test)
+      tho_acc = tho;
+      pho_acc = fo - mu_o * lg;
+    }
     if (!(th_t == th_t) || !(ph_t == ph_t)) ok = false;
     return ok;
   }
@@ -1015,6 +1338,180 @@ struct Solver {
     return v;
   }
 
+  // Filter backtracking line search (Waechter & Biegler 2006; IPOPT's order of tests): alpha = a0,
+  // a0/2, ... down to a_min, one second-order correction after the first rejected trial when it did
+  // not decrease theta; acceptance = theta_max, then the switching / Armijo or sufficient-decrease
+  // test against (th, ph, gphi), then the filter.  The accepted trial is in buffer 1-cur.  nls counts
+  // the halvings (in/out).
+  MR_HD bool backtrack(T a0, T ap, T th, T ph, T gphi, T a_min, T th_pow, T& alpha, bool& ftype, bool& rej_filter,
+                       int& nls) {
+    const T s_phi = T(2.3), delta_sw = T(1), eta = T(1e-4), g_th = T(1e-5), g_ph = T(1e-5);
+    (void)ap;
+    alpha = a0;
+    const int nls0 = nls;
+    // backtracking ends below a_min, or below 1e-30: a_min is 0 when theta is (and may flush to 0
+    // in fp32), and halving alpha to 0 would never leave the loop
+    while (alpha >= a_min && alpha >= T(1e-30)) {
+      for (int pass = 0; pass < 2; ++pass) {
+        bool soc = pass == 1;
+        T th_t, ph_t;
+        bool ok;
+        MR_PROF(3, ok = trial(alpha, soc, th_t, ph_t));
+        if (ok) ok = th_t <= theta_max;
+        if (ok) {
+          bool sw = gphi < T(0) && alpha * mr_exp(s_phi * mr_log(-gphi)) > delta_sw * th_pow;
+          if (th <= theta_min && sw) {
+            ok = ph_t <= ph + eta * alpha * gphi + T(1e-14) * mr_abs(ph);
+            ftype = true;
+          } else {
+            ok = th_t <= (T(1) - g_th) * th || ph_t <= ph - g_ph * th + T(1e-14) * mr_abs(ph);
+            ftype = false;
+          }
+        }
+        // the filter last (IPOPT's order: theta_max, sufficient decrease, then the filter), so a
+        // rejection by the filter itself is known for the reset heuristic
+        if (ok && !filter_ok(th_t, ph_t)) { ok = false; rej_filter = true; }
+        if (ok) return true;
+        // second-order correction only after the first rejected trial with theta not decreased (not in
+        // the restoration phase: its rows carry the relaxations p, n)
+        if (!(nls == nls0 && !soc && th_t >= th) || resto) break;
+      }
+      alpha *= T(0.5);
+      nls++;
+    }
+    return false;
+  }
+
+  // watchdog snapshot of the current iterate (buffer cur, multipliers) and search direction
+  MR_HD void wd_save() {
+    for (int k = 0; k <= N; ++k) {
+      for (int i = 0; i < NZS; ++i) { W(k, WF::WZ + i) = W(k, zf(cur) + i); W(k, WF::WDZ + i) = W(k, WF::DZ + i); }
+      for (int j = 0; j < NI; ++j) {
+        W(k, WF::WSL + j) = W(k, sf(cur) + j); W(k, WF::WLAM + j) = W(k, WF::LAM + j);
+        W(k, WF::WDS + j) = W(k, WF::DS + j); W(k, WF::WDLAM + j) = W(k, WF::DLAM + j);
+      }
+      for (int i = 0; i < NX; ++i) { W(k, WF::WNU + i) = W(k, WF::NUv + i); W(k, WF::WDNU + i) = W(k, WF::DNU + i); }
+    }
+  }
+  MR_HD void wd_restore() {
+    for (int k = 0; k <= N; ++k) {
+      for (int i = 0; i < NZS; ++i) { W(k, zf(cur) + i) = W(k, WF::WZ + i); W(k, WF::DZ + i) = W(k, WF::WDZ + i); }
+      for (int j = 0; j < NI; ++j) {
+        W(k, sf(cur) + j) = W(k, WF::WSL + j); W(k, WF::LAM + j) = W(k, WF::WLAM + j);
+        W(k, WF::DS + j) = W(k, WF::WDS + j); W(k, WF::DLAM + j) = W(k, WF::WDLAM + j);
+      }
+      for (int i = 0; i < NX; ++i) { W(k, WF::NUv + i) = W(k, WF::WNU + i); W(k, WF::DNU + i) = W(k, WF::WDNU + i); }
+    }
+  }
+
+  // ---------------- the restoration phase (IPOPT's l1 restoration, W&B 2006 sec. 3.3) ----------------
+  // Entered when the filter line search finds no acceptable step at an infeasible point (pr_max > tol).
+  // The restoration NLP relaxes every constraint of the reference NLP: the 6 vehicle dynamics rows of
+  // each stage (F - x' - p + n = 0) and every inequality row (d(z) - s - p + n = 0); the definitional rows
+  // of the restatement (S+ = S + dS, the previous-control copies) are not constraints of the reference:
+  //   min rho sum (p + n) + zeta/2 sum D^2 (z - z_R)^2,  p, n >= 0,
+  // rho = 1000, zeta = sqrt(mu), D = min(1, 1/|z_R|) on the reference's variables; solved by the same
+  // IPM (eval / Riccati / forward / filter line search with its own filter and barrier parameter,
+  // starting at max(mu, max violation)).  It returns to the original problem at the first accepted
+  // step whose point reduces the original theta to <= 0.9 theta(z_R) and is acceptable to the original
+  // filter (augmented with z_R's entry on entering).
+  MR_HD void resto_enter(T th, T ph) {
+    const T g_th = T(1e-5), g_ph = T(1e-5);
+    filter_add((T(1) - g_th) * th, ph - g_ph * th);
+    onfilt = nfilt;
+    for (int i = 0; i < FMAX; ++i) { ofilt_th[i] = filt_th[i]; ofilt_ph[i] = filt_ph[i]; }
+    mu_o = mu;
+    th_entry = th;
+    delta_last_o = delta_last;
+    theta_max_o = theta_max;
+    theta_min_o = theta_min;
+    const T mu_r = mr_max(mu, pr_max);
+    T th_rows = T(0);
+    for (int k = 0; k <= N; ++k) {
+      T z[NZS];
+      load_z(k, cur, z);
+      for (int i = 0; i < NZS; ++i) W(k, WF::RZ + i) = z[i];
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      T d[NI];
+      int act[NI];
+      Row<T> rows[NROW];
+      row_values(k, z, e, d, act, rows);
+      for (int j = 0; j < NI; ++j) {
+        T p = T(1), n = T(1);
+        if (act[j]) {
+          const T c = d[j] - W(k, sf(cur) + j);
+          th_rows += mr_abs(c);
+          resto_pn(c, mu_r, rho, p, n);
+        }
+        W(k, WF::RP + j) = p;
+        W(k, WF::RN + j) = n;
+        W(k, WF::RVP + j) = mu_r / p;
+        W(k, WF::RVN + j) = mu_r / n;
+        W(k, WF::RDP + j) = W(k, WF::RDN + j) = W(k, WF::RDVP + j) = W(k, WF::RDVN + j) = T(0);
+        W(k, WF::RY + j) = W(k, WF::RDY + j) = T(0);  // the rows' equality multipliers start at 0
+        W(k, WF::DLAM + j) = T(0);
+#ifndef MR_RESTO_LAMINIT
+#define MR_RESTO_LAMINIT 2
+#endif
+        if (act[j]) {
+          if (MR_RESTO_LAMINIT == 1) W(k, WF::LAM + j) = mr_min(W(k, WF::LAM + j), rho);
+          if (MR_RESTO_LAMINIT == 2) W(k, WF::LAM + j) = mu_r / W(k, sf(cur) + j);
+        }
+      }
+      for (int i = 0; i < NX; ++i) { W(k, WF::NUv + i) = T(0); W(k, WF::DNU + i) = T(0); }
+      if (k < N)
+        for (int i = 0; i < 6; ++i) {  // the vehicle rows start satisfied too (p - n = F - x')
+          T p, n;
+          const T c = W(k, WF::C + i);
+          th_rows += mr_abs(c);
+          resto_pn(c, mu_r, rho, p, n);
+          W(k, WF::CP + i) = p;
+          W(k, WF::CN + i) = n;
+          W(k, WF::CVP + i) = mu_r / p;
+          W(k, WF::CVN + i) = mu_r / n;
+          W(k, WF::CDP + i) = W(k, WF::CDN + i) = W(k, WF::CDVP + i) = W(k, WF::CDVN + i) = T(0);
+        }
+    }
+    alpha_p = alpha_d = T(0);
+    mu = mu_r;
+    resto = true;
+    nfilt = 0;
+    delta_last = T(0);
+    const T th_r = mr_max(theta - th_rows, T(0));  // relaxed rows start satisfied: the definitional rows only
+    theta_max = T(1e4) * mr_max(T(1), th_r);
+    theta_min = T(1e-4) * mr_max(T(1), th_r);
+  }
+  MR_HD bool resto_done() const {  // the accepted restoration step's point, seen by the original problem
+    if (!(tho_acc <= T(RESTO_KAPPA) * th_entry)) return false;
+    for (int i = 0; i < FMAX; ++i)
+      if (i < onfilt && tho_acc >= ofilt_th[i] && pho_acc >= ofilt_ph[i]) return false;
+    return true;
+  }
+  MR_HD void resto_exit() {
+    // bound multipliers: a Newton step for complementarity at the new point (mu/s), reset to 1 where it
+    // changes them by more than bound_mult_reset_threshold; equality multipliers reset to 0
+    // (constr_mult_reset_threshold = 0); IPOPT's barrier parameter, filter and perturbation state back
+    for (int k = 0; k <= N; ++k) {
+      for (int j = 0; j < NI; ++j) {
+        const T s = W(k, sf(cur) + j), lam = W(k, WF::LAM + j) + alpha_d * W(k, WF::DLAM + j);
+        T ln = mu_o / s;
+        if (mr_abs(ln - lam) > T(RESTO_MULT_RESET)) ln = T(1);
+        W(k, WF::LAM + j) = W(k, WF::LAM + j) == T(0) ? T(0) : ln;  // inactive slots stay 0
+        W(k, WF::DLAM + j) = T(0);
+      }
+      for (int i = 0; i < NX; ++i) { W(k, WF::NUv + i) = T(0); W(k, WF::DNU + i) = T(0); }
+    }
+    alpha_p = alpha_d = T(0);
+    mu = mu_o;
+    nfilt = onfilt;
+    for (int i = 0; i < FMAX; ++i) { filt_th[i] = ofilt_th[i]; filt_ph[i] = ofilt_ph[i]; }
+    theta_max = theta_max_o;
+    theta_min = theta_min_o;
+    delta_last = delta_last_o;
+    resto = false;
+  }
+
   // ---------------- the IPM loop ----------------
   MR_HD SolveOut solve() {
     const T kappa_eps = T(10), kappa_mu = T(0.2), theta_mu = T(1.5);
@@ -1027,6 +1524,10 @@ struct Solver {
     // IPOPT's filter reset heuristic (filter_reset_trigger = 5, max_filter_resets = 5): after this many
     // successive iterations whose line search had a trial point rejected by the filter, clear it
     int filt_rej_iters = 0, filt_resets = 0;
+    // watchdog state and the reference values of the point where it started
+    bool in_wd = false;
+    int wd_short = 0, wd_trial = 0;
+    T wd_th = T(0), wd_ph = T(0), wd_gphi = T(0), wd_ap = T(0), wd_ad = T(0), wd_amin = T(0), wd_thpow = T(0);
     int it = 0;
     for (it = 0;; ++it) {
       MR_PROF(0, eval_sweep(mu_prev));
@@ -1040,13 +1541,22 @@ struct Solver {
         }
       }
       T kkt = kkt_error(T(0));
-      out.kkt = (double)kkt;
-      out.obj = (double)(fval / sc);
       if (!(kkt == kkt) || !(fval == fval)) { out.status = 3; break; }
-      if (kkt <= P.tol) { out.status = 0; break; }
-      if (P.acc_iter > 0) {
-        acc_count = (kkt <= P.acc_tol) ? acc_count + 1 : 0;
-        if (acc_count >= P.acc_iter) { out.status = 1; break; }
+#ifdef MR_RESTO_DEBUG
+      if (trace) printf("it %d resto %d kkt %.3e stat %.3e pr %.3e smax %.3e smin %.3e nu1 %.3e lam1 %.3e mi %d mu %.3e fval %.6e theta %.4e\n", it, (int)resto, (double)kkt, (double)stat_max, (double)pr_max, (double)slam_max, (double)slam_min, (double)nu1, (double)lam1, mi, (double)mu, (double)fval, (double)theta);
+#endif
+      if (resto) {
+        // the restoration NLP converged at a point the original problem does not accept: IPOPT's
+        // "converged to a point of local infeasibility"
+        if (kkt <= P.tol) { out.status = MR_STATUS_INFEASIBLE; break; }
+      } else {
+        out.kkt = (double)kkt;
+        out.obj = (double)(fval / sc);
+        if (kkt <= P.tol) { out.status = 0; break; }
+        if (P.acc_iter > 0) {
+          acc_count = (kkt <= P.acc_tol) ? acc_count + 1 : 0;
+          if (acc_count >= P.acc_iter) { out.status = 1; break; }
+        }
       }
       if (it >= P.max_iter) { out.status = 2; break; }
       T mu_old = mu;
@@ -1054,7 +1564,11 @@ struct Solver {
         T m1 = kappa_mu * mu, m2 = mr_exp(theta_mu * mr_log(mu));
         mu = mr_max(mu_min, mr_min(m1, m2));
       }
-      if (mu != mu_old) nfilt = 0;
+      if (mu != mu_old) {  // IPOPT resets its line search with a new barrier problem: filter and watchdog
+        nfilt = 0;
+        in_wd = false;
+        wd_short = 0;
+      }
       // inertia-corrected factorisation
       T delta = T(0);
       bool first = true, fact_ok = false;
@@ -1075,8 +1589,8 @@ struct Solver {
       T ap, ad, gphi;
       MR_PROF(2, forward(ap, ad, gphi));
       // filter line search
-      const T th = theta, ph = fval - mu * logs;
-      const T th_pow = mr_exp(s_theta * mr_log(mr_max(th, T(1e-30))));
+      T th = theta, ph = fval - mu * logs;
+      T th_pow = mr_exp(s_theta * mr_log(mr_max(th, T(1e-30))));
       T a_min;
       if (gphi < T(0)) {
         T t1 = g_ph * th / (-gphi);
@@ -1085,48 +1599,108 @@ struct Solver {
       } else {
         a_min = T(0.05) * g_th;
       }
-      T alpha = ap;
-      bool accepted = false, ftype = false, rej_filter = false;
-      int nls = 0;
-      // backtracking ends below a_min, or below 1e-30: a_min is 0 when theta is (and may flush to 0
-      // in fp32), and halving alpha to 0 would never leave the loop
-      while (alpha >= a_min && alpha >= T(1e-30)) {
-        for (int pass = 0; pass < 2 && !accepted; ++pass) {
-          bool soc = pass == 1;
-          T th_t, ph_t;
-          bool ok;
-          MR_PROF(3, ok = trial(alpha, soc, th_t, ph_t));
-          if (ok) ok = th_t <= theta_max;
-          if (ok) {
-            bool sw = gphi < T(0) && alpha * mr_exp(s_phi * mr_log(-gphi)) > delta_sw * th_pow;
-            if (th <= theta_min && sw) {
-              ok = ph_t <= ph + eta * alpha * gphi + T(1e-14) * mr_abs(ph);
-              ftype = true;
-            } else {
-              ok = th_t <= (T(1) - g_th) * th || ph_t <= ph - g_ph * th + T(1e-14) * mr_abs(ph);
-              ftype = false;
-            }
+      if (resto) {  // a restoration-phase step: its own filter, no watchdog, no second-order correction
+        T alpha = ap;
+        bool ftype = false, rej_filter = false;
+        int nls = 0;
+        const bool accepted = backtrack(ap, ap, th, ph, gphi, a_min, th_pow, alpha, ftype, rej_filter, nls);
+        if (!accepted) { out.status = 3; break; }  // IPOPT: restoration failed
+        for (int k = 0; k <= N; ++k) {
+          for (int j = 0; j < NI; ++j) {
+            W(k, WF::RP + j) += alpha * W(k, WF::RDP + j);
+            W(k, WF::RN + j) += alpha * W(k, WF::RDN + j);
           }
-          // the filter last (IPOPT's order: theta_max, sufficient decrease, then the filter), so a
-          // rejection by the filter itself is known for the reset heuristic
-          if (ok && !filter_ok(th_t, ph_t)) { ok = false; rej_filter = true; }
-          if (ok) { accepted = true; break; }
-          // second-order correction only after the first rejected trial with theta not decreased
-          if (!(nls == 0 && !soc && th_t >= th)) break;
+          if (k < N)
+            for (int i = 0; i < 6; ++i) {
+              W(k, WF::CP + i) += alpha * W(k, WF::CDP + i);
+              W(k, WF::CN + i) += alpha * W(k, WF::CDN + i);
+            }
         }
-        if (accepted) break;
-        alpha *= T(0.5);
-        nls++;
+        if (!ftype) filter_add((T(1) - g_th) * th, ph - g_ph * th);
+        if (trace && it < trace_cap) {
+          double* tr = trace + 8 * it;
+          tr[0] = (double)kkt; tr[1] = (double)mu; tr[2] = (double)alpha; tr[3] = (double)ad;
+          tr[4] = (double)delta; tr[5] = (double)th; tr[6] = (double)tho_acc; tr[7] = -200.0 - nls;
+        }
+        alpha_p = alpha;
+        alpha_d = ad;
+        mu_prev = mu;
+        cur = 1 - cur;
+        if (resto_done()) {
+          resto_exit();
+          mu_prev = mu;
+          in_wd = false;
+          wd_short = 0;
+          acc_count = 0;
+          filt_rej_iters = 0;
+        }
+        continue;
       }
-      // no acceptable step: see mr_wave.h (same rule)
-      ls_fail = accepted ? 0 : ls_fail + 1;
+#if MR_WD_TRIGGER > 0
+      // IPOPT's watchdog (watchdog_shortened_iter_trigger, watchdog_trial_iter_max): after that many
+      // successive iterations whose accepted step was shorter than the fraction-to-boundary step, store
+      // the iterate and its search direction and take full steps tentatively; they are judged against
+      // the stored point, and after watchdog_trial_iter_max iterations without an acceptable one the
+      // solver returns to the stored point and backtracks along its direction (skipping the full step)
+      if (!in_wd && wd_short >= MR_WD_TRIGGER) {
+        wd_save();
+        wd_th = th; wd_ph = ph; wd_gphi = gphi; wd_ap = ap; wd_ad = ad; wd_amin = a_min; wd_thpow = th_pow;
+        in_wd = true;
+        wd_trial = 0;
+      }
+#endif
+      T alpha = ap;
+      bool accepted = false, ftype = false, rej_filter = false, take_anyway = false;
+      int nls = 0;
+      if (in_wd) {
+        accepted = backtrack(ap, ap, wd_th, wd_ph, wd_gphi, ap, wd_thpow, alpha, ftype, rej_filter, nls);
+        if (accepted) {
+          in_wd = false;
+          wd_short = 0;
+          th = wd_th; ph = wd_ph;  // the filter entry is the watchdog point's (the acceptor's reference)
+        } else if (++wd_trial <= MR_WD_TRIAL_MAX) {
+          take_anyway = true;  // the full step is taken tentatively (its trial is in buffer 1-cur)
+          alpha = ap;
+          T th_t, ph_t;
+          trial(alpha, false, th_t, ph_t);  // (re-)write the plain full-step point (the last trial may be a SOC)
+        } else {
+          // back to the watchdog point: its iterate and direction, a regular backtracking line search
+          // that skips the full step
+          wd_restore();
+          in_wd = false;
+          wd_short = 0;
+          th = wd_th; ph = wd_ph; gphi = wd_gphi; ap = wd_ap; ad = wd_ad; a_min = wd_amin; th_pow = wd_thpow;
+          alpha = T(0.5) * ap;
+          nls = 1;
+          accepted = backtrack(alpha, ap, th, ph, gphi, a_min, th_pow, alpha, ftype, rej_filter, nls);
+        }
+      } else {
+        accepted = backtrack(ap, ap, th, ph, gphi, a_min, th_pow, alpha, ftype, rej_filter, nls);
+      }
+      // no acceptable step at an infeasible point: the restoration phase (from the next iteration on)
+      if (!accepted && !take_anyway && pr_max > P.tol) {
+        resto_enter(th, ph);
+        mu_prev = mu;
+        in_wd = false;
+        wd_short = 0;
+        acc_count = 0;
+        if (trace && it < trace_cap) {
+          double* tr = trace + 8 * it;
+          tr[0] = (double)kkt; tr[1] = (double)mu; tr[2] = (double)0; tr[3] = (double)0;
+          tr[4] = (double)delta; tr[5] = (double)th; tr[6] = (double)ph; tr[7] = -300.0;
+        }
+        continue;
+      }
+      // no acceptable step at a point feasible to the tolerance: the shortest tried step (see mr_wave.h)
+      ls_fail = (accepted || take_anyway) ? 0 : ls_fail + 1;
       if (ls_fail >= MR_LS_FAIL_MAX) { out.status = 3; break; }
-      if (!accepted) {
+      if (!accepted && !take_anyway) {
         alpha = mr_min(mr_max(alpha, a_min), ap);
         T th_t, ph_t;
         trial(alpha, false, th_t, ph_t);
         ftype = false;
       }
+      if (!take_anyway) wd_short = (accepted && alpha < ap) ? wd_short + 1 : 0;
 #if MR_FILTER_RESET_TRIGGER > 0
       if (filt_resets < MR_MAX_FILTER_RESETS) {
         filt_rej_iters = rej_filter ? filt_rej_iters + 1 : 0;
@@ -1137,11 +1711,12 @@ struct Solver {
         }
       }
 #endif
-      if (!ftype) filter_add((T(1) - g_th) * th, ph - g_ph * th);
+      if (!ftype && !take_anyway) filter_add((T(1) - g_th) * th, ph - g_ph * th);
       if (trace && it < trace_cap) {
         double* tr = trace + 8 * it;
         tr[0] = (double)kkt; tr[1] = (double)mu; tr[2] = (double)alpha; tr[3] = (double)ad;
-        tr[4] = (double)delta; tr[5] = (double)th; tr[6] = (double)ph; tr[7] = (double)(accepted ? nls : -1);
+        tr[4] = (double)delta; tr[5] = (double)th; tr[6] = (double)ph;
+        tr[7] = (double)(take_anyway ? -100 - wd_trial : (accepted ? nls : -1));
       }
       alpha_p = alpha;
       alpha_d = ad;
