@@ -102,7 +102,53 @@ def cpu_baseline(name, batch, gpu_iters, budget_s):
             "cpu_model": _cpu_model(),
             "iters_mean_cpu_fp64": float(it.mean()), "iters_mean_gpu_same_instances": float(gpu_iters[:n].mean()),
             "latency_1core_ms": {"p50": float(np.median(lat)), "p90": float(np.quantile(lat, 0.9)),
-                                 "sample": "C1 + 100 C2 instances, one at a time, 1 thread"}}
+                                 "sample": "C1 + 100 C2 instances, one at a time, 1 thread"},
+            "other_configs": cpu_other_configs(budget_s)}
+
+
+def copy_bandwidth(dev, gib=1.0, reps=10):
+    """Measured device copy bandwidth (frac against a measured copy as well as
+    the 8 TB/s spec): torch's vectorised elementwise copy of a gib-GiB fp32 buffer into another, timed
+    with HIP events over reps launches; bytes moved = read + write."""
+    import torch
+    n = int(gib * (1 << 30)) // 4
+    a = torch.ones(n, dtype=torch.float32, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize(dev)
+    st = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record(st)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    del a, b
+    return 2.0 * n * 4 / (ms * 1e-3) / 1e9
+
+
+def cpu_other_configs(budget_s):
+    """Scalar C++ fp64 twin throughput on bounded samples of C2 and C3 (BASELINE.md §2 asks for the
+    C2 and C3 instance sets too): solves/s on this host's cores."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import host_twin as ht
+    from mpcracing import workload as wl
+    cores = _cpu_threads()
+    res = {}
+    for name, n in (("C2", 1024), ("C3", 32 * cores)):
+        cfg = wl.CONFIGS[name]
+        b = wl.make_batch(name, limit=n)
+        c = ht.config(cfg["N"], cfg["model"], "fp64", cfg["lane"], cfg["Ts"], tol=1e-8, acceptable_iter=15,
+                      acceptable_tol=1e-6)
+        t0 = time.perf_counter()
+        o = ht.solve(c, b, nthreads=cores, scalar=True)
+        dt = time.perf_counter() - t0
+        res[name] = {"value": n / dt, "unit": "solves/s", "instances": n, "seconds": dt,
+                     "solved_frac": float((o["status"] <= 1).mean()), "iters_mean": float(o["iters"].mean())}
+        if time.perf_counter() - t0 > budget_s:
+            break
+    return res
 
 
 def reduce_counters(counts, elapsed, world):
@@ -186,6 +232,9 @@ def main():
     ap.add_argument("--no-latency", action="store_true", help="skip the B = 1 latency probe (profiling runs)")
     ap.add_argument("--cpu-check", action="store_true", help="multi-rank plumbing on CPU (gloo), no solve")
     ap.add_argument("--dispatch-order", type=int, default=1, help="mr_config.dispatch_order (A/B runs)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU test of the rank plumbing of the real path (MR_BENCH_BACKEND=gloo): process group, "
+                         "shards, counter reduction and the JSON line, with the solves skipped (no GPU)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -203,51 +252,71 @@ def main():
     from mpcracing import workload as wl
     from mpcracing.batch import solver_for_config
 
+    # backend: RCCL ("nccl") on the GPU box; MR_BENCH_BACKEND=gloo with --dry-run drives this same path
+    # on CPU in tests/test_multirank.py
+    backend = os.environ.get("MR_BENCH_BACKEND", "nccl")
+    dry = args.dry_run
+    if dry and backend != "gloo":
+        raise SystemExit("--dry-run needs MR_BENCH_BACKEND=gloo (it is the CPU test of the rank plumbing)")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
-    else:
+        if dry:
+            dist.init_process_group(backend, rank=rank, world_size=world)
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend, rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    elif not dry:
         torch.cuda.set_device(0)
-    dev = torch.device("cuda", local)
+    dev = torch.device("cpu") if dry else torch.device("cuda", local)
     cfg = wl.CONFIGS[args.config]
     per = args.per_gpu or cfg["per_gpu"]
     batch = wl.make_batch(args.config, rank=rank, world=world, per_gpu=per)
     B = int(batch["s0"].shape[0])
-    solver = solver_for_config(args.config, B, device=local, dispatch_order=args.dispatch_order)
-    dev_in = solver.to_device(batch)
-    out = solver.alloc_outputs(B)
-    stream = torch.cuda.current_stream(dev)
-
-    for _ in range(args.warmup):
-        solver.launch(dev_in, out, stream)
-    torch.cuda.synchronize(dev)
-
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     W = 4 if cfg["precision"] == "fp32" else 8
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for s in range(args.steps):
-        starts[s].record(stream)
-        solver.launch(dev_in, out, stream)
-        ends[s].record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    # per-launch kernel durations (HIP events on the launch stream)
-    kms = [starts[s].elapsed_time(ends[s]) for s in range(args.steps)]
-    it = out["iters"].cpu().numpy()
-    stc = np.bincount(out["status"].cpu().numpy(), minlength=5)[:5]
+    if dry:  # no solve: zero iterations, every instance "solved", unit timings
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        kms = [1.0] * args.steps
+        it = np.zeros(B, dtype=np.int32)
+        stc = np.array([B, 0, 0, 0, 0])
+    else:
+        solver = solver_for_config(args.config, B, device=local, dispatch_order=args.dispatch_order)
+        dev_in = solver.to_device(batch)
+        out = solver.alloc_outputs(B)
+        stream = torch.cuda.current_stream(dev)
+
+        for _ in range(args.warmup):
+            solver.launch(dev_in, out, stream)
+        torch.cuda.synchronize(dev)
+
+        starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+        ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for s in range(args.steps):
+            starts[s].record(stream)
+            solver.launch(dev_in, out, stream)
+            ends[s].record(stream)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        # per-launch kernel durations (HIP events on the launch stream)
+        kms = [starts[s].elapsed_time(ends[s]) for s in range(args.steps)]
+        it = out["iters"].cpu().numpy()
+        stc = np.bincount(out["status"].cpu().numpy(), minlength=5)[:5]
     iters_launch = float(it.sum())            # one launch (every launch solves the same shard)
     alg_bytes = algorithmic_bytes(cfg["N"], W, it)
 
     # B = 1 latency (same configuration, first instance), p50 of 5 runs
     lat_b1_ms = None
-    if not args.no_latency:
+    if not args.no_latency and not dry:
         b1 = {k: (v[..., :1].copy() if v is not None else None) for k, v in batch.items()}
         s1 = solver_for_config(args.config, 1, device=local)
         d1 = s1.to_device(b1)
@@ -264,6 +333,10 @@ def main():
     tot, elapsed_max = reduce_counters(
         torch.tensor([B * args.steps, iters_launch, alg_bytes, B] + stc.tolist(), dtype=torch.float64, device=dev),
         elapsed, world)
+
+    copy_gbs = None
+    if rank == 0 and not dry:
+        copy_gbs = copy_bandwidth(dev)
 
     if rank == 0:
         solves = tot[0]
@@ -300,13 +373,19 @@ def main():
             "p50_latency_b1_ms": lat_b1_ms,
             "iters_mean": float(tot[1] / tot[3]),
             "status_hist": {"solved": int(tot[4]), "acceptable": int(tot[5]), "max_iter": int(tot[6]),
-                            "failed": int(tot[7]), "lane_infeasible": int(tot[8])},
+                            "failed": int(tot[7]), "infeasible": int(tot[8])},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "mr_wave_kernel", "avg_launch_ms": kavg * 1e3,
-                         "alg_bytes_per_launch": alg_bytes},
+                         "alg_bytes_per_launch": alg_bytes,
+                         "copy_gbs": copy_gbs,
+                         "frac_vs_copy": (achieved / copy_gbs) if copy_gbs else None,
+                         "copy_source": "measured in this run: 1 GiB fp32 device-to-device copy (torch copy_, "
+                                        "read + write bytes), HIP events"},
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if dry:
+            line["dry_run"] = True
+        if world == 1 and not args.no_cpu_baseline and not dry:
             line["cpu_baseline"] = cpu_baseline(args.config, batch, it, args.cpu_budget)
         print(json.dumps(line), flush=True)
     if world > 1:

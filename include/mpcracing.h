@@ -34,7 +34,7 @@ extern "C" {
 
 /* ABI version (mr_version()): bumped whenever a struct layout or an entry point's meaning changes, so
    a caller built against another header can refuse to run (101: mr_config.dispatch_order,
-   mr_outputs.lam_g / timeline, status 4 = restoration failed) */
+   mr_outputs.lam_g / timeline, mr_config without lane_penalty (hard lane rows), status 4 = infeasible) */
 #define MR_ABI_VERSION 101
 
 #define MR_OK 0
@@ -79,7 +79,6 @@ typedef struct mr_config {
   double Ts;           /* sampling time */
   double tol;          /* KKT tolerance of the scaled NLP (IPOPT tol) */
   double acceptable_tol;
-  double lane_penalty; /* exact-penalty weight of the elastic lane rows (cost per metre of violation) */
   /* FixedControllerParameters (control/ControllerParameters.py:3-23) */
   double lambda_s, alpha_L, min_steer, max_steer, min_throttle, max_steer_delta, min_steer_delta,
       max_throttle_delta, min_throttle_delta, q_v_max, v_max, min_s_delta;

@@ -76,7 +76,7 @@ static int pointer_device(const void* p, int* dev) {
 // of that instance (mr_wave.h); the grid is the batch.
 // Waves per SIMD (launch bounds): fp32 2 -- the sweeps fit 256 registers with few spills (the
 // generated dynamics code built without SLP vectorisation, build.py), and a second resident wave
-// hides part of each instance's serial latency (C4 80.3 -> 78.4 ms, profiles/r02_flags_ab.json);
+// hides part of each instance's serial latency (A/B: profiles/r03_flags_ab.json, tools/gpu_flags_ab.sh);
 // fp64 1 -- its sweeps need the full 512-register file (C3 0.418 vs 0.389 s at 2 vs 1 in round 1).
 #ifndef MR_WAVES_PER_SIMD_F32
 #define MR_WAVES_PER_SIMD_F32 2
@@ -110,7 +110,8 @@ __global__ __launch_bounds__(WL, sizeof(T) == 4 ? MR_WAVES_PER_SIMD_F32 : MR_WAV
   // one solver object per lane (its wave-uniform iteration state), also in LDS
   constexpr bool SSL = SSInLDS<T>::value;
   __shared__ alignas(16) char slots[WL * sizeof(WaveSolver<T, MODEL, SSL>)];
-  __shared__ T filt_sh[2 * FMAX];  // the line-search filter, shared by the wave
+  __shared__ WaveShared<T> wsh;  // the line-search filter and the watchdog / restoration state, shared by the wave
+  T* const filt_sh = wsh.filt;
   if constexpr (SSL) {
     __shared__ T ssl[SS_WORDS];
     solve_instance_wave<T, MODEL, true, true>(P, in, out, B, i, wsi, (MR_LDS T*)lds, w, (MR_LDS T*)ssl, &Ish,

@@ -12,7 +12,6 @@ MR_HD void fill_params(const mr_config& c, const TyreCoef<double>& tf, const Tyr
   P.model = c.model;
   P.lane = c.lane_bounds;
   P.Ts = T(c.Ts);
-  P.lane_pen = T(c.lane_penalty);
   P.lambda_s = T(c.lambda_s); P.alpha_L = T(c.alpha_L);
   P.min_steer = T(c.min_steer); P.max_steer = T(c.max_steer); P.min_thr = T(c.min_throttle);
   P.max_dsteer = T(c.max_steer_delta); P.min_dsteer = T(c.min_steer_delta);
@@ -131,7 +130,6 @@ inline void fill_default_config(mr_config* c) {
   c->Ts = 0.05;
   c->tol = 1e-8;
   c->acceptable_tol = 1e-6;
-  c->lane_penalty = 1e5;
   c->lambda_s = 300; c->alpha_L = 500;
   c->min_steer = -0.9; c->max_steer = 0.9; c->min_throttle = -1.0;
   c->max_steer_delta = 0.2; c->min_steer_delta = -0.2;

@@ -34,7 +34,7 @@ namespace mr {
 enum ModelId { MODEL_KIN = 0, MODEL_DYN = 1, MODEL_BLEND = 2, MODEL_BLEND_PACEJKA = 3, MODEL_DYN_PACEJKA = 4 };
 
 constexpr int NX = 11, NU = 3, NZ = 14, NROW = 7, NI = 17;
-constexpr int NZS = NZ + 1;  // stored stage vector: z plus the elastic lane variable t (index 14)
+constexpr int NZS = NZ + 1;  // stored stage vector: z plus one unused slot (index 14, always 0)
 constexpr int JL = 14;       // slots 14, 15, 16: lane rows e_C + m + t >= 0, m - e_C + t >= 0, t >= 0
 constexpr int NH = NZ * (NZ + 1) / 2;  // packed upper triangle of the 14x14 stage Hessian
 constexpr int NP = NX * (NX + 1) / 2;  // packed P
@@ -71,7 +71,7 @@ MR_HD int pidx(int i, int j) {  // packed upper index of symmetric NX x NX
 template <typename T>
 struct ProbParams {
   int N, model, lane;
-  T Ts, lane_pen;  // elastic lane rows: exact-penalty weight (unscaled cost per metre)
+  T Ts;
   // control/ControllerParameters.py FixedControllerParameters
   T lambda_s, alpha_L, min_steer, max_steer, min_thr, max_dsteer, min_dsteer, max_dthr, min_dthr, q_vmax, v_max,
       min_ds;
@@ -268,18 +268,14 @@ MR_HD void make_row(const ProbParams<T>& P, const Inst<T>& I, int k, int r, cons
   }
 }
 
-// Lane rows on states i = 1..N (the commented MPC.py:135), elastic form:
-//   e_C + m + t >= 0,  m - e_C + t >= 0,  t >= 0, cost lane_pen * t (exact penalty: t* = 0
-//   and the same KKT point as the hard row whenever that NLP is feasible and lane_pen > |lambda*|).
+// Lane rows on states i = 1..N (the commented MPC.py:135), two one-sided rows as the reference's
+// opti.bounded(-max_error, e_hat_C, max_error): e_C + m >= 0, m - e_C >= 0.  An infeasible start is the
+// restoration phase's business (IPOPT's way), not an elastic reformulation.
 template <typename T>
 MR_HD bool lane_active(const ProbParams<T>& P, int k) { return P.lane && k >= 1; }
-// lane_pen > 0: the elastic form below; otherwise the hard rows e_C + m >= 0, m - e_C >= 0 of the
-// reference (t fixed at 0, row JL + 2 inactive), whose infeasible starts the restoration phase handles
-template <typename T>
-MR_HD bool lane_elastic(const ProbParams<T>& P) { (void)P; return false; }
 
 template <typename T>
-MR_HD void lane_d(const Inst<T>& I, T eC, T t, T* d) {
+MR_HD void lane_d(const Inst<T>& I, T eC, T t, T* d) {  // t: the unused slot 14 (0)
   d[0] = eC + I.max_err + t;
   d[1] = I.max_err - eC + t;
   d[2] = t;
@@ -685,7 +681,7 @@ struct Solver {
     }
     const int la = lane_active(P, k) ? 1 : 0;
     act[JL] = act[JL + 1] = la;
-    act[JL + 2] = la && lane_elastic(P);
+    act[JL + 2] = 0;  // (slot JL + 2 unused)
     lane_d(I, e.eC, z[14], d + JL);
   }
 
@@ -709,13 +705,13 @@ struct Solver {
       }
       Err<T> e;
       errors(I, z[0], z[1], z[6], e, false);
-      z[14] = lane_active(P, k) && lane_elastic(P) ? mr_max(mr_abs(e.eC) - I.max_err, T(0)) + T(1e-2) : T(0);
+      z[14] = T(0);
       store_z(k, 0, z);
 #ifdef MR_DEBUG_PRINT
       if (trace) printf("init k=%d vx=%g readback=%g X=%g S=%g\n", k, (double)z[3], (double)W(k, WF::Z0 + 3),
                         (double)z[0], (double)z[6]);
 #endif
-      // objective gradient for the gradient-based scaling (elastic variables excluded)
+      // objective gradient for the gradient-based scaling
       T g[NZ];
       for (int i = 0; i < NZ; ++i) g[i] = T(0);
       stage_cost(P, I, k, z, e, T(1), g, (T*)nullptr);
@@ -759,21 +755,6 @@ struct Solver {
     theta_max = T(1e4) * mr_max(T(1), th);
     theta_min = T(1e-4) * mr_max(T(1), th);
     nfilt = 0;
-  }
-
-  // Elastic lane variable: condensed 1x1 block of the stage Newton system.
-  //   h_tt = sum sig_j, h_tz = (sig_0 - sig_1) grad(eC), g_t = sc*pen + sum_j (sig_j r_j - mu/s_j)
-  MR_HD void lane_block(int k, int b, const T* d, T& htt, T& hd, T& gt0, T& gt1) const {
-    htt = T(0); gt0 = sc * P.lane_pen; gt1 = T(0);
-    T sig[3];
-    for (int q = 0; q < 3; ++q) {
-      T s = W(k, sf(b) + JL + q), lam = W(k, WF::LAM + JL + q);
-      sig[q] = lam / s;
-      htt += sig[q];
-      gt0 += sig[q] * (d[JL + q] - s);
-      gt1 -= T(1) / s;
-    }
-    hd = sig[0] - sig[1];  // h_tz = hd * grad(eC)
   }
 
   // ---------------- sweep 1: evaluation, KKT error, stage QP data ----------------
@@ -1374,7 +1355,7 @@ struct Solver {
         if (ok) return true;
         // second-order correction only after the first rejected trial with theta not decreased (not in
         // the restoration phase: its rows carry the relaxations p, n)
-        if (!(nls == nls0 && !soc && th_t >= th) || resto) break;
+        if (!(nls == 0 && !soc && th_t >= th) || resto) break;
       }
       alpha *= T(0.5);
       nls++;

@@ -92,7 +92,38 @@ struct RCF {
 };
 constexpr int RC_STRIDE = 336;  // words; 16-word (64 B) multiple
 static_assert(RCF::NF <= RC_STRIDE, "record");
-constexpr int64_t WS_WORDS = (int64_t)SSF::NF * WL + (int64_t)RC_STRIDE * WL;
+// Cold per-stage fields [f][64] after the records: touched only by the watchdog (its snapshot of the
+// iterate and the search direction) and the restoration phase (the relaxations p, n of the rows and
+// of the 6 vehicle dynamics rows, their bound duals and steps, the rows' equality multipliers y, the
+// reference point z_R, the condensed disturbance weights of the Riccati sweep) -- same meaning as the
+// WF fields of mr_solver.h's scalar solver.
+struct CSF {
+  enum {
+    WZ = 0, WSL = WZ + NZS, WLAM = WSL + NI, WNU = WLAM + NI, WDZ = WNU + NX, WDS = WDZ + NZS, WDLAM = WDS + NI,
+    WDNU = WDLAM + NI,
+    RP = WDNU + NX, RN = RP + NI, RVP = RN + NI, RVN = RVP + NI, RDP = RVN + NI, RDN = RDP + NI, RDVP = RDN + NI,
+    RDVN = RDVP + NI, RY = RDVN + NI, RDY = RY + NI, RZ = RDY + NI,
+    CP = RZ + NZS, CN = CP + 6, CVP = CN + 6, CVN = CVP + 6, CDP = CVN + 6, CDN = CDP + 6, CDVP = CDN + 6,
+    CDVN = CDVP + 6, CSW = CDVN + 6, CGW0 = CSW + 6, CGW1 = CGW0 + 6, NF = CGW1 + 6
+  };
+};
+constexpr int64_t WS_WORDS = (int64_t)SSF::NF * WL + (int64_t)RC_STRIDE * WL + (int64_t)CSF::NF * WL;
+
+// Wave-uniform state of the watchdog and the restoration phase: one copy per wavefront next to the
+// line-search filter (LDS on the device), every lane writing the same values -- not in the per-lane
+// solver objects, whose LDS footprint sets the occupancy.
+template <typename T>
+struct WaveCold {
+  int resto, in_wd, wd_short, wd_trial, onfilt;
+  T rho, zeta, mu_o, th_entry, delta_last_o, theta_max_o, theta_min_o, tho, pho;
+  T wd_th, wd_ph, wd_gphi, wd_ap, wd_ad, wd_amin, wd_thpow;
+  T ofilt[2 * FMAX];  // the original problem's filter while the restoration phase runs
+};
+template <typename T>
+struct WaveShared {
+  T filt[2 * FMAX];
+  WaveCold<T> cold;
+};
 constexpr int LDS_LD = 17;  // padded row of the 16 x 16 LDS tiles
 constexpr int LX_OFF = 0, LP_OFF = 16 * LDS_LD, LDX_OFF = 32 * LDS_LD;
 constexpr int LJUNK_OFF = LDX_OFF + WL * 12;  // one discard slot per lane (branch-free stores)
@@ -199,11 +230,14 @@ struct WaveSolver {
   T theta_max, theta_min;
 #if MR_DEVICE_BUILD
   // the filter is wave-uniform: one copy per workgroup in LDS (set by mr_wave_kernel), every
-  // lane writing the same values, instead of one copy per lane in the solver object
+  // lane writing the same values, instead of one copy per lane in the solver object; the
+  // watchdog / restoration state (WaveCold) follows it in the same LDS block (WaveShared)
   MR_LDS T* filt;
+  MR_HD MR_LDS WaveCold<T>* cw() const { return &((MR_LDS WaveShared<T>*)filt)->cold; }
 #else
-  T filt_store[2 * FMAX];
-  T* filt = filt_store;
+  WaveShared<T> sh_store;
+  T* filt = sh_store.filt;
+  MR_HD WaveCold<T>* cw() { return &sh_store.cold; }
 #endif
   int nfilt;
   T stat_max, pr_max, theta, slam_max, slam_min, nu1, lam1, fval, logs;
@@ -223,6 +257,7 @@ struct WaveSolver {
       : P(P_), I(I_), w(w_), ss(ss_), rc(ws + (int64_t)SSF::NF * WL), lds(lds_), N(P_.N), ln(w_.lane) {}
 
   MR_HD auto& S(int f) const { return ss[f * WL + ln]; }
+  MR_HD MR_GLOBAL T& Cf(int f) const { return rc[(int64_t)RC_STRIDE * WL + f * WL + ln]; }  // cold field
   MR_HD auto& fth(int i) const { return filt[i]; }
   MR_HD auto& fph(int i) const { return filt[FMAX + i]; }
   MR_HD MR_GLOBAL T* R(int k) const { return rc + (int64_t)k * RC_STRIDE; }
@@ -250,22 +285,9 @@ struct WaveSolver {
       d[2 * r + 1] = hi - c;
     }
     const int la = lane_active(P, k) ? 1 : 0;
-    act[JL] = act[JL + 1] = act[JL + 2] = la;
-    lane_d(I, e.eC, z[14], d + JL);
-  }
-
-  MR_HD void lane_block(int b, const T* d, T& htt, T& hd, T& gt0, T& gt1) const {
-    MR_UNIFORM_P();
-    htt = T(0); gt0 = sc * P.lane_pen; gt1 = T(0);
-    T sig[3];
-    for (int q = 0; q < 3; ++q) {
-      T s = S(sf(b) + JL + q), lam = S(SSF::LAM + JL + q);
-      sig[q] = lam / s;
-      htt += sig[q];
-      gt0 += sig[q] * (d[JL + q] - s);
-      gt1 -= T(1) / s;
-    }
-    hd = sig[0] - sig[1];
+    act[JL] = act[JL + 1] = la;  // the hard lane rows e_C + m >= 0, m - e_C >= 0 (slot JL + 2 unused)
+    act[JL + 2] = 0;
+    lane_d(I, e.eC, T(0), d + JL);
   }
 
   // ---------------- initialisation (MPC.py:100-131) ----------------
@@ -288,7 +310,7 @@ struct WaveSolver {
       }
       Err<T> e;
       errors(I, z[0], z[1], z[6], e, false);
-      z[14] = lane_active(P, k) ? mr_max(mr_abs(e.eC) - I.max_err, T(0)) + T(1e-2) : T(0);
+      z[14] = T(0);  // (the stage vector's slot 14 is unused)
       if (ln == k)
         for (int i = 0; i < NZS; ++i) my[i] = z[i];
       if (k < N) {
@@ -353,13 +375,28 @@ struct WaveSolver {
     theta_max = T(1e4) * mr_max(T(1), th);
     theta_min = T(1e-4) * mr_max(T(1), th);
     nfilt = 0;
+    auto* C = cw();
+    C->resto = 0;
+    C->in_wd = 0;
+    C->wd_short = 0;
+    C->wd_trial = 0;
   }
 
   // ---------------- sweep 1: evaluation, KKT error terms, stage QP data (lane = stage) ----------------
+  // RESTO: the restoration phase's NLP (mr_solver.h Solver::eval_sweep with resto set): relaxed vehicle
+  // dynamics and rows, the proximity term instead of the objective
+  template <bool RESTO>
   MR_SWEEP void eval_sweep(T mu_prev) {
     MR_ASSUME_LDS_STATE();
     MR_UNIFORM_P();
     const T kappa_sigma = T(1e10);
+    T rho = T(0), zeta = T(0);
+    if constexpr (RESTO) {
+      rho = cw()->rho;
+      zeta = mr_sqrt(mu_prev);  // IPOPT: resto_proximity_weight sqrt(mu)
+      cw()->zeta = zeta;
+    }
+    auto clip = [&](T v, T x) { return mr_min(mr_max(v, mu_prev / (kappa_sigma * x)), kappa_sigma * mu_prev / x); };
     const int k = ln;
     T st_l = T(0), pr_l = T(0), th_l = T(0), smax_l = T(0), smin_l = T(1e30), nu1_l = T(0), lam1_l = T(0),
       f_l = T(0), lg_l = T(0);
@@ -377,16 +414,6 @@ struct WaveSolver {
     }
     T z[NZS];
     load_z(cur, z);
-#if MR_EVAL_HOIST
-    // the slacks and multipliers of every row loaded with the iterate, ahead of the record stores
-    // (otherwise the compiler must keep them behind those stores: a second memory round trip)
-    T s_in[NI], lam_in[NI], dlam_in[NI];
-    for (int j = 0; j < NI; ++j) {
-      s_in[j] = own() ? S(sf(cur) + j) : T(1);
-      lam_in[j] = own() ? S(SSF::LAM + j) : T(0);
-      dlam_in[j] = own() ? S(SSF::DLAM + j) : T(0);
-    }
-#endif
     T nun[NX], znext[NX];
     for (int i = 0; i < NX; ++i) {
       nun[i] = wshfl(w, nuk[i], nxt());
@@ -417,6 +444,27 @@ struct WaveSolver {
         c[8] = z[12] - znext[8];
         c[9] = (k == 0 ? z[11] : z[9]) - znext[9];
         c[10] = (k == 0 ? z[12] : z[10]) - znext[10];
+        if constexpr (RESTO) {  // relaxed vehicle rows F - x' - p + n (the S / previous-control rows are definitions)
+          for (int i = 0; i < 6; ++i) {
+            const T p = Cf(CSF::CP + i), n = Cf(CSF::CN + i);
+            const T vp = clip(Cf(CSF::CVP + i) + alpha_d * Cf(CSF::CDVP + i), p);
+            const T vn = clip(Cf(CSF::CVN + i) + alpha_d * Cf(CSF::CDVN + i), n);
+            Cf(CSF::CVP + i) = vp;
+            Cf(CSF::CVN + i) = vn;
+            c[i] += n - p;
+            const T ip = p / vp, in = n / vn, sw = T(1) / (ip + in);
+            Cf(CSF::CSW + i) = sw;
+            Cf(CSF::CGW0 + i) = sw * rho * (in - ip);
+            Cf(CSF::CGW1 + i) = sw * (T(1) / vp - T(1) / vn);
+            smax_l = mr_max(smax_l, mr_max(p * vp, n * vn));
+            smin_l = mr_min(smin_l, mr_min(p * vp, n * vn));
+            lam1_l += mr_abs(vp) + mr_abs(vn);
+            lg_l += mr_log(p) + mr_log(n);
+            mi_l += 2;
+            f_l += rho * (p + n);
+            st_l = mr_max(st_l, mr_max(mr_abs(rho - nun[i] - vp), mr_abs(rho + nun[i] - vn)));
+          }
+        }
         for (int i = 0; i < NX; ++i) {
           rbe.st(c[i], 0u, Rk + RCF::C + i);
           pr_l = mr_max(pr_l, mr_abs(c[i]));
@@ -431,7 +479,13 @@ struct WaveSolver {
       }
       Err<T> e;
       errors(I, z[0], z[1], z[6], e, true);
-      f_l += stage_cost(P, I, k, z, e, sc, gl, H);
+      if constexpr (RESTO) {
+        T zr[NZS];
+        for (int i = 0; i < NZS; ++i) zr[i] = Cf(CSF::RZ + i);
+        f_l += prox_term(I, k, N, z, zr, zeta, gl, H);
+      } else {
+        f_l += stage_cost(P, I, k, z, e, sc, gl, H);
+      }
       for (int i = 0; i < NZ; ++i) { g0[i] += gl[i]; st[i] += gl[i]; S(SSF::GL + i) = gl[i]; }
       if (k >= 1)
         for (int i = 0; i < NX; ++i) st[i] -= nuk[i];
@@ -439,30 +493,47 @@ struct WaveSolver {
       int act[NI];
       row_values(k, z, e, d, act);
       T lam_j[NI], s_j[NI];
+      T sg_j[NI], c0_j[NI], c1_j[NI], y_j[NI];  // restoration: condensed row data (row_cond_r), multipliers y
       for (int j = 0; j < NI; ++j) {
         lam_j[j] = T(0);
         s_j[j] = T(1);
+        sg_j[j] = c0_j[j] = c1_j[j] = y_j[j] = T(0);
         if (!act[j]) continue;
-#if MR_EVAL_HOIST
-        T s = s_in[j];
-        T lam = lam_in[j] + alpha_d * dlam_in[j];
-#else
         T s = S(sf(cur) + j);
         T lam = S(SSF::LAM + j) + alpha_d * S(SSF::DLAM + j);
-#endif
         lam = mr_min(mr_max(lam, mu_prev / (kappa_sigma * s)), kappa_sigma * mu_prev / s);
         S(SSF::LAM + j) = lam;
         lam_j[j] = lam;
         s_j[j] = s;
         T rd = d[j] - s;
-        pr_l = mr_max(pr_l, mr_abs(rd));
-        th_l += mr_abs(rd);
         T sl = s * lam;
         smax_l = mr_max(smax_l, sl);
         smin_l = mr_min(smin_l, sl);
         lam1_l += mr_abs(lam);
         lg_l += mr_log(s);
         mi_l += 1;
+        if constexpr (RESTO) {  // relaxed row d - s - p + n; its multiplier y is its own variable (IPOPT's y_d)
+          const T p = Cf(CSF::RP + j), n = Cf(CSF::RN + j);
+          const T vp = clip(Cf(CSF::RVP + j) + alpha_d * Cf(CSF::RDVP + j), p);
+          const T vn = clip(Cf(CSF::RVN + j) + alpha_d * Cf(CSF::RDVN + j), n);
+          Cf(CSF::RVP + j) = vp;
+          Cf(CSF::RVN + j) = vn;
+          const T y = Cf(CSF::RY + j) + alpha_p * Cf(CSF::RDY + j);
+          Cf(CSF::RY + j) = y;
+          y_j[j] = y;
+          st_l = mr_max(st_l, mr_abs(y - lam));
+          rd = rd - p + n;
+          smax_l = mr_max(smax_l, mr_max(p * vp, n * vn));
+          smin_l = mr_min(smin_l, mr_min(p * vp, n * vn));
+          lam1_l += mr_abs(vp) + mr_abs(vn);
+          lg_l += mr_log(p) + mr_log(n);
+          mi_l += 2;
+          f_l += rho * (p + n);
+          st_l = mr_max(st_l, mr_max(mr_abs(rho + y - vp), mr_abs(rho - y - vn)));
+          row_cond_r(d[j], s, lam, p, n, vp, vn, rho, sg_j[j], c0_j[j], c1_j[j]);
+        }
+        pr_l = mr_max(pr_l, mr_abs(rd));
+        th_l += mr_abs(rd);
       }
 #pragma unroll
       for (int r = 0; r < NROW; ++r) {
@@ -471,12 +542,19 @@ struct WaveSolver {
 #pragma unroll
         for (int sd = 0; sd < 2; ++sd) {
           int j = 2 * r + sd;
-          T sig = lam_j[j] / s_j[j];
           T sgn = sd == 0 ? T(1) : T(-1);
-          sig_sum += sig;
-          gsc0 += sgn * sig * (d[j] - s_j[j]);
-          gsc1 += -sgn / s_j[j];
-          lamdiff += sgn * lam_j[j];
+          if constexpr (RESTO) {
+            sig_sum += sg_j[j];
+            gsc0 += sgn * c0_j[j];
+            gsc1 += sgn * c1_j[j];
+            lamdiff += sgn * y_j[j];
+          } else {
+            T sig = lam_j[j] / s_j[j];
+            sig_sum += sig;
+            gsc0 += sgn * sig * (d[j] - s_j[j]);
+            gsc1 += -sgn / s_j[j];
+            lamdiff += sgn * lam_j[j];
+          }
         }
 #pragma unroll
         for (int a = 0; a < RN(r); ++a) {
@@ -489,25 +567,28 @@ struct WaveSolver {
         }
       }
       if (lane_active(P, k)) {
+        // hard lane rows e_C + m >= 0 (slot JL) and m - e_C >= 0 (JL + 1), nonlinear in (X, Y, S)
         const int id3[3] = {0, 1, 6};
         T s0 = s_j[JL], s1 = s_j[JL + 1];
         T sig0 = lam_j[JL] / s0, sig1 = lam_j[JL + 1] / s1;
         T lamdiff = lam_j[JL] - lam_j[JL + 1];
         T gz0 = sig0 * (d[JL] - s0) - sig1 * (d[JL + 1] - s1);
         T gz1 = -T(1) / s0 + T(1) / s1;
-        T htt, hd, gt0, gt1;
-        lane_block(cur, d, htt, hd, gt0, gt1);
+        if constexpr (RESTO) {
+          sig0 = sg_j[JL];
+          sig1 = sg_j[JL + 1];
+          lamdiff = y_j[JL] - y_j[JL + 1];
+          gz0 = c0_j[JL] - c0_j[JL + 1];
+          gz1 = c1_j[JL] - c1_j[JL + 1];
+        }
         int q = 0;
         for (int a = 0; a < 3; ++a) {
-          g0[id3[a]] += e.gC[a] * (gz0 - hd * gt0 / htt);
-          g1[id3[a]] += e.gC[a] * (gz1 - hd * gt1 / htt);
+          g0[id3[a]] += e.gC[a] * gz0;
+          g1[id3[a]] += e.gC[a] * gz1;
           st[id3[a]] -= lamdiff * e.gC[a];
           for (int bb = a; bb < 3; ++bb, ++q)
-            H[hidx(id3[a], id3[bb])] += (sig0 + sig1 - hd * hd / htt) * e.gC[a] * e.gC[bb] - lamdiff * e.hC[q];
+            H[hidx(id3[a], id3[bb])] += (sig0 + sig1) * e.gC[a] * e.gC[bb] - lamdiff * e.hC[q];
         }
-        f_l += sc * P.lane_pen * z[14];
-        T stt = sc * P.lane_pen - lam_j[JL] - lam_j[JL + 1] - lam_j[JL + 2];
-        st_l = mr_max(st_l, mr_abs(stt));
       }
       if (k >= 1)
         for (int i = 0; i < NX; ++i) st_l = mr_max(st_l, mr_abs(st[i]));
@@ -636,6 +717,42 @@ struct WaveSolver {
   // P, p0, p1, K, k0, k1 of stage k; the forward recursion forms A dx + B du + c from the stage's
   // Jacobian itself (no closed-loop map is stored: 132 fewer words written per stage and
   // factorisation, and a smaller record).
+  // Restoration phase: the cost-to-go tile P^ of stage k+1 (LP) minimised over the disturbance of
+  // stage k's relaxed vehicle rows (mr_solver.h noise_cond): M = P_vv + diag(sw) = L L^T (every lane,
+  // registers), Y = L^-1 [P_v. | p0_v + gw0 | p1_v + gw1] (lane c < 13: column c, to the LX scratch
+  // tile), then P^ -= Y^T Y entry-wise.  False if M is not positive definite.
+  MR_HD bool noise_tile(int k, MR_LDS T* LP) const {
+    MR_LDS T* const LX = lds + LX_OFF;
+    const MR_GLOBAL T* cb = rc + (int64_t)RC_STRIDE * WL;
+    const int l = ln;
+    T sw[6], gw0[6], gw1[6], M[36], L[36];
+    for (int i = 0; i < 6; ++i) {
+      sw[i] = cb[(CSF::CSW + i) * WL + k];
+      gw0[i] = cb[(CSF::CGW0 + i) * WL + k];
+      gw1[i] = cb[(CSF::CGW1 + i) * WL + k];
+    }
+    for (int i = 0; i < 6; ++i)
+      for (int j = 0; j < 6; ++j) M[i * 6 + j] = LP[i * LDS_LD + j] + (i == j ? sw[i] : T(0));
+    const bool ok = chol6(M, L);
+    if (!wuni(w, ok)) return false;
+    const int c = l < 13 ? l : 0;
+    T col[6];
+    for (int i = 0; i < 6; ++i) col[i] = LP[i * LDS_LD + c] + (c == 11 ? gw0[i] : (c == 12 ? gw1[i] : T(0)));
+    lsolve6(L, col);
+    if (l < 13)
+      for (int a = 0; a < 6; ++a) LX[a * 16 + l] = col[a];
+    wsync_lds(w);
+    for (int e = l; e < NX * 13; e += WL) {
+      const int i = e / 13, j = e - 13 * (e / 13);
+      T v = LP[i * LDS_LD + j];
+      for (int a = 0; a < 6; ++a) v -= LX[a * 16 + i] * LX[a * 16 + j];
+      LP[i * LDS_LD + j] = v;
+    }
+    wsync_lds(w);
+    return true;
+  }
+
+  template <bool RESTO>
   MR_SWEEP bool riccati(T delta, T /*mu*/) {
     MR_ASSUME_LDS_STATE();
     const int l = ln, N = wu(w, this->N), g = l >> 4, c = l & 15;
@@ -686,6 +803,8 @@ struct WaveSolver {
     // one stage; the loop below is unrolled by three so the prefetch buffers rotate roles
     // (no register copies of in-flight loads, hence exact vmcnt waits instead of vmcnt(0))
     auto step = [&](int k, const T* raw_use, T* raw_fill) -> bool {
+      bool noise_ok = true;
+      if constexpr (RESTO) noise_ok = noise_tile(k, LP);  // P^ of stage k+1 minimised over the disturbance
       // stage offsets as visibly wave-uniform values (SGPR soffsets, not per-lane waterfall loops)
       const unsigned Rk = (unsigned)wu(w, (int)R(k));
       T eb[4], dq[4];
@@ -753,7 +872,7 @@ struct WaveSolver {
         LP[fp.lp2[v]] = pv;
       }
       wsync_lds(w);
-      return piv_ok;
+      return piv_ok & noise_ok;
     };
     // Pivots are tested once per three stages, at the loop latch: a failed stage only costs the
     // next two, and the loop keeps one back-edge block (exact prefetch waits at the loop head).
@@ -922,15 +1041,9 @@ struct WaveSolver {
       dz[14] = T(0);
       adz[JL] = adz[JL + 1] = adz[JL + 2] = T(0);
       if (lane_active(P, k)) {
-        T htt, hd, gt0, gt1;
-        lane_block(cur, d, htt, hd, gt0, gt1);
-        T gdz = e.gC[0] * dz[0] + e.gC[1] * dz[1] + e.gC[2] * dz[6];
-        T dt = -(hd * gdz + gt0 + mu * gt1) / htt;
-        dz[14] = dt;
-        adz[JL] = gdz + dt;
-        adz[JL + 1] = -gdz + dt;
-        adz[JL + 2] = dt;
-        g_l += sc * P.lane_pen * dt;
+        const T gdz = e.gC[0] * dz[0] + e.gC[1] * dz[1] + e.gC[2] * dz[6];
+        adz[JL] = gdz;
+        adz[JL + 1] = -gdz;
       }
       for (int i = 0; i < NZS; ++i) S(SSF::DZ + i) = dz[i];
       for (int j = 0; j < NI; ++j) {
@@ -953,6 +1066,135 @@ struct WaveSolver {
 #endif
   }
 
+  // ---------------- sweep 3 of the restoration phase ----------------
+  // The recursion is mr_solver.h Solver::forward with resto set, run wave-uniformly (every lane computes
+  // the same dx, du, disturbance; lane k keeps stage k's), the record read with uniform addresses --
+  // the restoration phase is entered by few instances for few iterations, so this sweep is written for
+  // clarity rather than for the prefetch pipeline of forward().  Then stage-parallel: the relaxed rows'
+  // and dynamics rows' steps (row_steps_r, dyn_steps_r), step limits, the directional derivative.
+  MR_SWEEP void forward_resto(T& ap, T& ad, T& gphi) {
+    MR_UNIFORM_P();
+    MR_ASSUME_LDS_STATE();
+    const T mu = this->mu, rho = cw()->rho;
+    const T tau = mr_max(T(0.99), T(1) - mu);
+    const int N = wu(w, this->N);
+    const MR_GLOBAL T* cb = rc + (int64_t)RC_STRIDE * WL;
+    T dx[NX], mydz[NZS], myw[6];
+    for (int i = 0; i < NX; ++i) dx[i] = T(0);
+    for (int i = 0; i < NZS; ++i) mydz[i] = T(0);
+    for (int i = 0; i < 6; ++i) myw[i] = T(0);
+    for (int k = 0; k <= N; ++k) {
+      const MR_GLOBAL T* Rk = R(k);
+      T du[NU] = {T(0), T(0), T(0)};
+      if (k < N)
+        for (int a = 0; a < NU; ++a) {
+          T v = Rk[RCF::K0 + a] + mu * Rk[RCF::K1 + a];
+          for (int j = 0; j < NX; ++j) v += Rk[RCF::K + a * NX + j] * dx[j];
+          du[a] = v;
+        }
+      if (ln == k) {
+        for (int i = 0; i < NX; ++i) mydz[i] = dx[i];
+        for (int a = 0; a < NU; ++a) mydz[NX + a] = du[a];
+      }
+      if (k == N) break;
+      T J[48], t[NX], tb[NX];
+      for (int i = 0; i < 48; ++i) J[i] = Rk[RCF::J + i];
+      apply_A(J, k, dx, t);
+      apply_B(J, k, du, tb);
+      for (int i = 0; i < NX; ++i) dx[i] = t[i] + tb[i] + Rk[RCF::C + i];
+      // + the disturbance of the relaxed vehicle rows, w = -M^-1 (nu_y + gw)
+      const MR_GLOBAL T* Rn = R(k + 1);
+      T Pn[NP], sw[6], rhs[6], wv[6];
+      for (int i = 0; i < NP; ++i) Pn[i] = Rn[RCF::P + i];
+      for (int i = 0; i < 6; ++i) {
+        T v = Rn[RCF::PV0 + i] + mu * Rn[RCF::PV1 + i];
+        for (int l = 0; l < NX; ++l) v += Pn[pidx(i, l)] * dx[l];
+        rhs[i] = v + cb[(CSF::CGW0 + i) * WL + k] + mu * cb[(CSF::CGW1 + i) * WL + k];
+        sw[i] = cb[(CSF::CSW + i) * WL + k];
+      }
+      noise_step(Pn, sw, rhs, wv);
+      for (int i = 0; i < 6; ++i) dx[i] += wv[i];
+      if (ln == k)
+        for (int i = 0; i < 6; ++i) myw[i] = wv[i];
+      // costate nu_{k+1} = P_{k+1} dx_{k+1} + p_{k+1}
+      if (ln == k + 1)
+        for (int i = 0; i < NX; ++i) {
+          T v = Rn[RCF::PV0 + i] + mu * Rn[RCF::PV1 + i];
+          for (int l = 0; l < NX; ++l) v += Pn[pidx(i, l)] * dx[l];
+          S(SSF::DNU + i) = v - S(SSF::NU + i);
+        }
+    }
+    T ap_l = T(1), ad_l = T(1), g_l = T(0);
+    if (own()) {
+      const int k = ln;
+      T dz[NZS];
+      for (int i = 0; i < NZS; ++i) dz[i] = mydz[i];
+      for (int i = 0; i < NZ; ++i) g_l += S(SSF::GL + i) * dz[i];
+      T z[NZS];
+      load_z(cur, z);
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      T d[NI];
+      int act[NI];
+      row_values(k, z, e, d, act);
+      T adz[NI];
+#pragma unroll
+      for (int r = 0; r < NROW; ++r) {
+        const T v = row_c(r, dz);
+        adz[2 * r] = v;
+        adz[2 * r + 1] = -v;
+      }
+      dz[14] = T(0);
+      adz[JL] = adz[JL + 1] = adz[JL + 2] = T(0);
+      if (lane_active(P, k)) {
+        const T gdz = e.gC[0] * dz[0] + e.gC[1] * dz[1] + e.gC[2] * dz[6];
+        adz[JL] = gdz;
+        adz[JL + 1] = -gdz;
+      }
+      for (int i = 0; i < NZS; ++i) S(SSF::DZ + i) = dz[i];
+      for (int j = 0; j < NI; ++j) {
+        if (!act[j]) continue;
+        const T s = S(sf(cur) + j), lam = S(SSF::LAM + j);
+        const T p = Cf(CSF::RP + j), n = Cf(CSF::RN + j), vp = Cf(CSF::RVP + j), vn = Cf(CSF::RVN + j);
+        T ds, dl, dp, dn, dvp, dvn;
+        row_steps_r(adz[j] + (d[j] - s - p + n), s, lam, p, n, vp, vn, rho, mu, ds, dp, dn, dl, dvp, dvn);
+        Cf(CSF::RDP + j) = dp;
+        Cf(CSF::RDN + j) = dn;
+        Cf(CSF::RDVP + j) = dvp;
+        Cf(CSF::RDVN + j) = dvn;
+        Cf(CSF::RDY + j) = lam + dl - Cf(CSF::RY + j);  // eta - y
+        S(SSF::DS + j) = ds;
+        S(SSF::DLAM + j) = dl;
+        g_l += (rho - mu / p) * dp + (rho - mu / n) * dn - mu * ds / s;
+        if (ds < T(0)) ap_l = mr_min(ap_l, -tau * s / ds);
+        if (dp < T(0)) ap_l = mr_min(ap_l, -tau * p / dp);
+        if (dn < T(0)) ap_l = mr_min(ap_l, -tau * n / dn);
+        if (dl < T(0)) ad_l = mr_min(ad_l, -tau * lam / dl);
+        if (dvp < T(0)) ad_l = mr_min(ad_l, -tau * vp / dvp);
+        if (dvn < T(0)) ad_l = mr_min(ad_l, -tau * vn / dvn);
+      }
+      if (k < N)
+        for (int i = 0; i < 6; ++i) {
+          const T p = Cf(CSF::CP + i), n = Cf(CSF::CN + i), vp = Cf(CSF::CVP + i), vn = Cf(CSF::CVN + i);
+          T dp, dn, dvp, dvn;
+          dyn_steps_r(myw[i], p, n, vp, vn, rho, mu, dp, dn, dvp, dvn);
+          Cf(CSF::CDP + i) = dp;
+          Cf(CSF::CDN + i) = dn;
+          Cf(CSF::CDVP + i) = dvp;
+          Cf(CSF::CDVN + i) = dvn;
+          g_l += (rho - mu / p) * dp + (rho - mu / n) * dn;
+          if (dp < T(0)) ap_l = mr_min(ap_l, -tau * p / dp);
+          if (dn < T(0)) ap_l = mr_min(ap_l, -tau * n / dn);
+          if (dvp < T(0)) ad_l = mr_min(ad_l, -tau * vp / dvp);
+          if (dvn < T(0)) ad_l = mr_min(ad_l, -tau * vn / dvn);
+        }
+    }
+    ap = wmin(w, ap_l);
+    ad = wmin(w, ad_l);
+    gphi = wsum(w, g_l);
+    wsync(w);  // costate steps of every lane written
+  }
+
   // ---------------- sweep 4: the filter line search (IPOPT backtracking, one SOC) ----------------
   // The lane's stage iterate, step, slacks and slack steps are loaded once; every trial point is
   // formed and measured in registers (one pass per trial: the trial's stage values, its dynamics
@@ -962,7 +1204,14 @@ struct WaveSolver {
   // alpha = ap, ap/2, ... down to a_min; a second-order correction only after the first trial
   // (nls = 0) when it did not decrease theta; acceptance = theta_max, then the switching /
   // Armijo or sufficient-decrease test, then the filter.
-  MR_SWEEP void line_search(T th, T ph, T gphi, T ap, T a_min, T th_pow) {
+  // a0: the first trial step (ap, or ap/2 when the watchdog backtracks from its stored point, nls0 = 1:
+  // the full step was tried); ap: the fraction-to-boundary step (the fallback point's upper clamp)
+  // RESTO: the restoration phase's line search (mr_solver.h trial() with resto set): the relaxations
+  // p, n of the rows and of the vehicle dynamics rows move with the step; theta and phi of the
+  // restoration NLP decide, the point's original theta / barrier objective go to the WaveCold state
+  // (the restoration exit test); no second-order correction.
+  template <bool RESTO>
+  MR_SWEEP void line_search(T th, T ph, T gphi, T a0, T ap, T a_min, T th_pow, int nls0) {
     MR_UNIFORM_P();
     MR_ASSUME_LDS_STATE();
     const T s_phi = T(2.3), delta_sw = T(1), eta = T(1e-4), g_th = T(1e-5), g_ph = T(1e-5);
@@ -980,11 +1229,34 @@ struct WaveSolver {
       row_bounds(P, I, k, r, a, lo, hi);
       actm |= (own() && a) ? (3u << (2 * r)) : 0u;
     }
-    actm |= (own() && lane_active(P, k)) ? (7u << JL) : 0u;
+    actm |= (own() && lane_active(P, k)) ? (3u << JL) : 0u;
     for (int j = 0; j < NI; ++j) {
       const bool a = (actm >> j) & 1u;
       s_c[j] = a ? S(sf(cur) + j) : T(1);
       ds[j] = a ? S(SSF::DS + j) : T(0);
+    }
+    // restoration: the relaxations and their steps (rows of this stage; vehicle rows of x_{k+1})
+    T rp[NI], rn[NI], rdp[NI], rdn[NI], cp[6], cn[6], cdp[6], cdn[6], zr[NZS];
+    T rho = T(0), zeta = T(0), mu_o = T(0);
+    if constexpr (RESTO) {
+      rho = cw()->rho;
+      zeta = cw()->zeta;
+      mu_o = cw()->mu_o;
+      for (int j = 0; j < NI; ++j) {
+        const bool a = (actm >> j) & 1u;
+        rp[j] = a ? Cf(CSF::RP + j) : T(1);
+        rn[j] = a ? Cf(CSF::RN + j) : T(1);
+        rdp[j] = a ? Cf(CSF::RDP + j) : T(0);
+        rdn[j] = a ? Cf(CSF::RDN + j) : T(0);
+      }
+      const bool dk = own() && k < N;
+      for (int i = 0; i < 6; ++i) {
+        cp[i] = dk ? Cf(CSF::CP + i) : T(1);
+        cn[i] = dk ? Cf(CSF::CN + i) : T(1);
+        cdp[i] = dk ? Cf(CSF::CDP + i) : T(0);
+        cdn[i] = dk ? Cf(CSF::CDN + i) : T(0);
+      }
+      for (int i = 0; i < NZS; ++i) zr[i] = own() ? Cf(CSF::RZ + i) : T(0);
     }
     T zt[NZS], st[NI];
     // one trial point: zt, st (registers), theta, phi; false if a slack is not positive or a value is
@@ -1018,7 +1290,7 @@ struct WaveSolver {
       }
       T ztn[NX];
       for (int i = 0; i < NX; ++i) ztn[i] = wshfl(w, zt[i], nxt());
-      T th_l = T(0), f_l = T(0), lg_l = T(0);
+      T th_l = T(0), f_l = T(0), lg_l = T(0), lgr_l = T(0), tho_l = T(0), fo_l = T(0);
       int ok_l = 1;
       if (own()) {
         Err<T> e, ep;
@@ -1038,26 +1310,59 @@ struct WaveSolver {
           if (soc) sj += d[j] - dp[j];
           if (!(sj > T(0))) ok_l = 0;
           st[j] = sj;
-          th_l += mr_abs(d[j] - sj);
           lg_l += mr_log(sj > T(0) ? sj : T(1));
+          if constexpr (RESTO) {
+            const T pt = rp[j] + alpha * rdp[j], nt = rn[j] + alpha * rdn[j];
+            if (!(pt > T(0)) || !(nt > T(0))) ok_l = 0;
+            th_l += mr_abs(d[j] - sj - pt + nt);
+            tho_l += mr_abs(d[j] - sj);
+            lgr_l += mr_log(pt > T(0) ? pt : T(1)) + mr_log(nt > T(0) ? nt : T(1));
+            f_l += rho * (pt + nt);
+          } else {
+            th_l += mr_abs(d[j] - sj);
+          }
         }
-        f_l += stage_cost(P, I, k, zt, e, sc, (T*)nullptr, (T*)nullptr);
-        if (lane_active(P, k)) f_l += sc * P.lane_pen * zt[14];
+        if constexpr (RESTO) {
+          f_l += prox_term(I, k, N, zt, zr, zeta, (T*)nullptr, (T*)nullptr);
+          fo_l += stage_cost(P, I, k, zt, e, sc, (T*)nullptr, (T*)nullptr);
+        } else {
+          f_l += stage_cost(P, I, k, zt, e, sc, (T*)nullptr, (T*)nullptr);
+        }
         if (k < N && !soc) {
           T xn[NX];
           faug<T, MODEL>(P, k, zt, xn);
-          for (int i = 0; i < NX; ++i) th_l += mr_abs(xn[i] - ztn[i]);
+          if constexpr (RESTO) {
+            for (int i = 0; i < NX; ++i) {
+              T r = xn[i] - ztn[i];
+              tho_l += mr_abs(r);
+              if (i < 6) {  // the relaxed vehicle rows
+                const T pt = cp[i] + alpha * cdp[i], nt = cn[i] + alpha * cdn[i];
+                if (!(pt > T(0)) || !(nt > T(0))) ok_l = 0;
+                r += nt - pt;
+                lgr_l += mr_log(pt > T(0) ? pt : T(1)) + mr_log(nt > T(0) ? nt : T(1));
+                f_l += rho * (pt + nt);
+              }
+              th_l += mr_abs(r);
+            }
+          } else {
+            for (int i = 0; i < NX; ++i) th_l += mr_abs(xn[i] - ztn[i]);
+          }
         }
       }
       th_t = wsum(w, th_l);
       const T fv = wsum(w, f_l), lg = wsum(w, lg_l);
       int ok = wmin(w, ok_l);
       ph_t = fv - mu * lg;
+      if constexpr (RESTO) {
+        ph_t = fv - mu * (lg + wsum(w, lgr_l));
+        cw()->tho = wsum(w, tho_l);  // the point as the original problem sees it (restoration exit test)
+        cw()->pho = wsum(w, fo_l) - mu_o * lg;
+      }
       if (!(th_t == th_t) || !(ph_t == ph_t)) ok = 0;
       return wuni(w, ok != 0);
     };
-    T alpha = ap;
-    int nls = 0, pass = 0, ntr = 0, nsoc = 0;
+    T alpha = a0;
+    int nls = nls0, pass = 0, ntr = 0, nsoc = 0;
     bool accepted = false, ftype = false, rej_filter = false;
     // backtracking ends below a_min, or below 1e-30: a_min is 0 when theta is (and may flush to 0 in
     // fp32), and halving alpha to 0 would never leave the loop.  No acceptable step: IPOPT would enter
@@ -1087,7 +1392,7 @@ struct WaveSolver {
       // heuristic
       if (ok && !filter_ok(th_t, ph_t)) { ok = false; rej_filter = true; }
       if (wuni(w, ok)) { accepted = true; break; }
-      if (pass == 0 && nls == 0 && th_t >= th) { pass = 1; continue; }  // second-order correction
+      if (!RESTO && pass == 0 && nls == 0 && th_t >= th) { pass = 1; continue; }  // second-order correction
       pass = 0;
       alpha *= T(0.5);
       nls++;
@@ -1100,6 +1405,20 @@ struct WaveSolver {
       for (int j = 0; j < NI; ++j)
         if ((actm >> j) & 1u) S(sf(nb) + j) = st[j];
       for (int i = 0; i < NZS; ++i) S(zf(nb) + i) = zt[i];
+      if constexpr (RESTO) {  // the relaxations move in place (their step is applied once, here)
+        if (accepted) {
+          for (int j = 0; j < NI; ++j)
+            if ((actm >> j) & 1u) {
+              Cf(CSF::RP + j) = rp[j] + alpha * rdp[j];
+              Cf(CSF::RN + j) = rn[j] + alpha * rdn[j];
+            }
+          if (k < N)
+            for (int i = 0; i < 6; ++i) {
+              Cf(CSF::CP + i) = cp[i] + alpha * cdp[i];
+              Cf(CSF::CN + i) = cn[i] + alpha * cdn[i];
+            }
+        }
+      }
     }
     res_alpha = alpha;
     res_flags = (accepted ? 1 : 0) | (ftype ? 2 : 0) | (rej_filter ? 4 : 0);
@@ -1130,6 +1449,134 @@ struct WaveSolver {
     T v = T(0);
     if (P.lane && own() && ln >= 1) v = S(zf(cur) + 14);
     return wmax(w, v);
+  }
+
+  // ---------------- watchdog snapshot (lane = stage) ----------------
+  MR_SWEEP void wd_save() {
+    MR_ASSUME_LDS_STATE();
+    if (own()) {
+      for (int i = 0; i < NZS; ++i) { Cf(CSF::WZ + i) = S(zf(cur) + i); Cf(CSF::WDZ + i) = S(SSF::DZ + i); }
+      for (int j = 0; j < NI; ++j) {
+        Cf(CSF::WSL + j) = S(sf(cur) + j); Cf(CSF::WLAM + j) = S(SSF::LAM + j);
+        Cf(CSF::WDS + j) = S(SSF::DS + j); Cf(CSF::WDLAM + j) = S(SSF::DLAM + j);
+      }
+      for (int i = 0; i < NX; ++i) { Cf(CSF::WNU + i) = S(SSF::NU + i); Cf(CSF::WDNU + i) = S(SSF::DNU + i); }
+    }
+    wsync(w);
+  }
+  MR_SWEEP void wd_restore() {
+    MR_ASSUME_LDS_STATE();
+    if (own()) {
+      for (int i = 0; i < NZS; ++i) { S(zf(cur) + i) = Cf(CSF::WZ + i); S(SSF::DZ + i) = Cf(CSF::WDZ + i); }
+      for (int j = 0; j < NI; ++j) {
+        S(sf(cur) + j) = Cf(CSF::WSL + j); S(SSF::LAM + j) = Cf(CSF::WLAM + j);
+        S(SSF::DS + j) = Cf(CSF::WDS + j); S(SSF::DLAM + j) = Cf(CSF::WDLAM + j);
+      }
+      for (int i = 0; i < NX; ++i) { S(SSF::NU + i) = Cf(CSF::WNU + i); S(SSF::DNU + i) = Cf(CSF::WDNU + i); }
+    }
+    wsync(w);
+  }
+
+  // ---------------- the restoration phase (mr_solver.h Solver::resto_enter / resto_done / resto_exit) ----------------
+  MR_SWEEP void resto_enter(T th, T ph) {
+    MR_UNIFORM_P();
+    MR_ASSUME_LDS_STATE();
+    const T g_th = T(1e-5), g_ph = T(1e-5), rho = T(RESTO_RHO);
+    auto* C = cw();
+    filter_add((T(1) - g_th) * th, ph - g_ph * th);
+    C->onfilt = nfilt;
+    for (int i = 0; i < 2 * FMAX; ++i) C->ofilt[i] = filt[i];
+    C->mu_o = mu;
+    C->th_entry = th;
+    C->delta_last_o = delta_last;
+    C->theta_max_o = theta_max;
+    C->theta_min_o = theta_min;
+    C->rho = rho;
+    const T mu_r = mr_max(mu, pr_max);
+    T th_rows_l = T(0);
+    if (own()) {
+      const int k = ln;
+      T z[NZS];
+      load_z(cur, z);
+      for (int i = 0; i < NZS; ++i) Cf(CSF::RZ + i) = z[i];
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      T d[NI];
+      int act[NI];
+      row_values(k, z, e, d, act);
+      for (int j = 0; j < NI; ++j) {
+        T p = T(1), n = T(1);
+        if (act[j]) {
+          const T s = S(sf(cur) + j), c = d[j] - s;
+          th_rows_l += mr_abs(c);
+          resto_pn(c, mu_r, rho, p, n);
+          S(SSF::LAM + j) = mu_r / s;  // the slacks' bound duals restart at complementarity with mu_R
+        }
+        Cf(CSF::RP + j) = p;
+        Cf(CSF::RN + j) = n;
+        Cf(CSF::RVP + j) = mu_r / p;
+        Cf(CSF::RVN + j) = mu_r / n;
+        Cf(CSF::RDP + j) = T(0); Cf(CSF::RDN + j) = T(0); Cf(CSF::RDVP + j) = T(0); Cf(CSF::RDVN + j) = T(0);
+        Cf(CSF::RY + j) = T(0);  // the rows' equality multipliers start at 0
+        Cf(CSF::RDY + j) = T(0);
+        S(SSF::DLAM + j) = T(0);
+      }
+      for (int i = 0; i < NX; ++i) { S(SSF::NU + i) = T(0); S(SSF::DNU + i) = T(0); }
+      if (k < N)
+        for (int i = 0; i < 6; ++i) {  // the vehicle rows start satisfied too (p - n = F - x')
+          T p, n;
+          const T c = R(k)[RCF::C + i];
+          th_rows_l += mr_abs(c);
+          resto_pn(c, mu_r, rho, p, n);
+          Cf(CSF::CP + i) = p;
+          Cf(CSF::CN + i) = n;
+          Cf(CSF::CVP + i) = mu_r / p;
+          Cf(CSF::CVN + i) = mu_r / n;
+          Cf(CSF::CDP + i) = T(0); Cf(CSF::CDN + i) = T(0); Cf(CSF::CDVP + i) = T(0); Cf(CSF::CDVN + i) = T(0);
+        }
+    }
+    const T th_rows = wsum(w, th_rows_l);
+    alpha_p = alpha_d = T(0);
+    mu = mu_r;
+    C->resto = 1;
+    nfilt = 0;
+    delta_last = T(0);
+    const T th_r = mr_max(theta - th_rows, T(0));  // relaxed rows start satisfied: the definitional rows only
+    theta_max = T(1e4) * mr_max(T(1), th_r);
+    theta_min = T(1e-4) * mr_max(T(1), th_r);
+    wsync(w);
+  }
+  MR_HD bool resto_done() {  // the accepted restoration step's point, seen by the original problem
+    auto* C = cw();
+    const T tho = C->tho, pho = C->pho;
+    bool ok = tho <= T(RESTO_KAPPA) * C->th_entry;
+    for (int i = 0; i < FMAX; ++i)
+      if (i < C->onfilt && tho >= C->ofilt[i] && pho >= C->ofilt[FMAX + i]) ok = false;
+    return wuni(w, ok);
+  }
+  MR_SWEEP void resto_exit() {
+    MR_ASSUME_LDS_STATE();
+    auto* C = cw();
+    const T mu_o = C->mu_o;
+    if (own()) {
+      for (int j = 0; j < NI; ++j) {
+        const T s = S(sf(cur) + j), lam0 = S(SSF::LAM + j), lam = lam0 + alpha_d * S(SSF::DLAM + j);
+        T lnew = mu_o / s;
+        if (mr_abs(lnew - lam) > T(RESTO_MULT_RESET)) lnew = T(1);
+        S(SSF::LAM + j) = lam0 == T(0) ? T(0) : lnew;  // inactive slots stay 0
+        S(SSF::DLAM + j) = T(0);
+      }
+      for (int i = 0; i < NX; ++i) { S(SSF::NU + i) = T(0); S(SSF::DNU + i) = T(0); }
+    }
+    alpha_p = alpha_d = T(0);
+    mu = mu_o;
+    nfilt = C->onfilt;
+    for (int i = 0; i < 2 * FMAX; ++i) filt[i] = C->ofilt[i];
+    theta_max = C->theta_max_o;
+    theta_min = C->theta_min_o;
+    delta_last = C->delta_last_o;
+    C->resto = 0;
+    wsync(w);
   }
 
   // ---------------- the IPM loop (wave-uniform control) ----------------
@@ -1164,17 +1611,25 @@ struct WaveSolver {
       // batch's slowest instances (which set its makespan) are not slowed by the short ones
       if (it == MR_PRIO_ITER) __builtin_amdgcn_s_setprio(3);
 #endif
+      // wave-uniform mode of this iteration: the original problem, or its restoration phase
+      const bool rs = wuni(w, cw()->resto != 0);
       MR_T0();
-      eval_sweep(mu_prev);
+      if (rs) eval_sweep<true>(mu_prev); else eval_sweep<false>(mu_prev);
       MR_T1(0);
       T kkt = kkt_error(T(0));
-      out.kkt = (double)kkt;
-      out.obj = (double)(fval / sc);
       if (!(kkt == kkt) || !(fval == fval)) { out.status = 3; break; }
-      if (kkt <= P.tol) { out.status = 0; break; }
-      if (P.acc_iter > 0) {
-        acc_count = (kkt <= P.acc_tol) ? acc_count + 1 : 0;
-        if (acc_count >= P.acc_iter) { out.status = 1; break; }
+      if (rs) {
+        // the restoration NLP converged at a point the original problem does not accept: IPOPT's
+        // "converged to a point of local infeasibility"
+        if (kkt <= P.tol) { out.status = MR_STATUS_INFEASIBLE; break; }
+      } else {
+        out.kkt = (double)kkt;
+        out.obj = (double)(fval / sc);
+        if (kkt <= P.tol) { out.status = 0; break; }
+        if (P.acc_iter > 0) {
+          acc_count = (kkt <= P.acc_tol) ? acc_count + 1 : 0;
+          if (acc_count >= P.acc_iter) { out.status = 1; break; }
+        }
       }
       if (it >= P.max_iter) { out.status = 2; break; }
       T mu_old = mu;
@@ -1182,7 +1637,11 @@ struct WaveSolver {
         T m1 = kappa_mu * mu, m2 = mr_exp(theta_mu * mr_log(mu));
         mu = mr_max(mu_min, mr_min(m1, m2));
       }
-      if (mu != mu_old) nfilt = 0;
+      if (mu != mu_old) {  // IPOPT resets its line search with a new barrier problem: filter and watchdog
+        nfilt = 0;
+        cw()->in_wd = 0;
+        cw()->wd_short = 0;
+      }
       T delta = T(0);
       bool first = true, fact_ok = false;
       MR_T0();
@@ -1190,11 +1649,11 @@ struct WaveSolver {
         MR_CNT(6);
 #if MR_PHASE_CYCLES
         const unsigned long long tr0 = trace ? MR_CLOCK() : 0ull;
-        const bool rok = riccati(delta, mu);
+        const bool rok = rs ? riccati<true>(delta, mu) : riccati<false>(delta, mu);
         if (trace && !rok) { tsub[4] += MR_CLOCK() - tr0; tsub[5] += 1; }
         if (rok) { fact_ok = true; break; }
 #else
-        if (riccati(delta, mu)) { fact_ok = true; break; }
+        if (rs ? riccati<true>(delta, mu) : riccati<false>(delta, mu)) { fact_ok = true; break; }
 #endif
         if (first) {
           delta = delta_last == T(0) ? T(1e-4) : mr_max(T(1e-20), delta_last / T(3));
@@ -1209,10 +1668,10 @@ struct WaveSolver {
       if (delta > T(0)) delta_last = delta;
       T &ap = res_ap, &ad = res_ad, &gphi = res_gphi;
       MR_T0();
-      forward(ap, ad, gphi);
+      if (rs) forward_resto(ap, ad, gphi); else forward(ap, ad, gphi);
       MR_T1(2);
-      const T th = theta, ph = fval - mu * logs;
-      const T th_pow = mr_exp(s_theta * mr_log(mr_max(th, T(1e-30))));
+      T th = theta, ph = fval - mu * logs;
+      T th_pow = mr_exp(s_theta * mr_log(mr_max(th, T(1e-30))));
       T a_min;
       if (gphi < T(0)) {
         T t1 = g_ph * th / (-gphi);
@@ -1221,20 +1680,97 @@ struct WaveSolver {
       } else {
         a_min = T(0.05) * g_th;
       }
+      if (rs) {  // a restoration-phase step: its own filter, no watchdog, no second-order correction
+        MR_T0();
+        line_search<true>(th, ph, gphi, ap, ap, a_min, th_pow, 0);
+        MR_T1(3);
+        if (!(res_flags & 1)) { out.status = 3; break; }  // IPOPT: restoration failed
+        if (!(res_flags & 2)) filter_add((T(1) - g_th) * th, ph - g_ph * th);
+        if (trace && ln == 0 && it < trace_cap - 2) {
+          double* tr = trace + 8 * it;
+          tr[0] = (double)kkt; tr[1] = (double)mu; tr[2] = (double)res_alpha; tr[3] = (double)ad;
+          tr[4] = (double)delta; tr[5] = (double)th; tr[6] = (double)cw()->tho; tr[7] = -200.0 - res_nls;
+        }
+        alpha_p = res_alpha;
+        alpha_d = ad;
+        mu_prev = mu;
+        cur = 1 - cur;
+        wsync(w);
+        if (resto_done()) {
+          resto_exit();
+          mu_prev = mu;
+          cw()->in_wd = 0;
+          cw()->wd_short = 0;
+          acc_count = 0;
+          filt_rej_iters = 0;
+        }
+        continue;
+      }
+#if MR_WD_TRIGGER > 0
+      // IPOPT's watchdog (mr_solver.h, same rule): after watchdog_shortened_iter_trigger successive
+      // shortened steps store the iterate and direction, take full steps tentatively, judged against the
+      // stored point; after watchdog_trial_iter_max without an acceptable one, back to the stored point
+      if (!cw()->in_wd && cw()->wd_short >= MR_WD_TRIGGER) {
+        wd_save();
+        auto* C = cw();
+        C->wd_th = th; C->wd_ph = ph; C->wd_gphi = gphi; C->wd_ap = ap; C->wd_ad = ad; C->wd_amin = a_min;
+        C->wd_thpow = th_pow;
+        C->in_wd = 1;
+        C->wd_trial = 0;
+      }
+#endif
+      bool take_anyway = false;
       MR_T0();
-      line_search(th, ph, gphi, ap, a_min, th_pow);
+      if (wuni(w, cw()->in_wd != 0)) {
+        auto* C = cw();
+        line_search<false>(C->wd_th, C->wd_ph, C->wd_gphi, ap, ap, ap, C->wd_thpow, 0);
+        if (res_flags & 1) {
+          C->in_wd = 0;
+          C->wd_short = 0;
+          th = C->wd_th;  // the filter entry is the watchdog point's (the acceptor's reference)
+          ph = C->wd_ph;
+        } else if (++C->wd_trial <= MR_WD_TRIAL_MAX) {
+          take_anyway = true;  // the line search stored the plain full step (its fallback point at ap)
+        } else {
+          // back to the watchdog point: its iterate and direction, a regular backtracking line search
+          // that skips the full step
+          wd_restore();
+          C->in_wd = 0;
+          C->wd_short = 0;
+          th = C->wd_th; ph = C->wd_ph; gphi = C->wd_gphi; ap = C->wd_ap; ad = C->wd_ad; a_min = C->wd_amin;
+          th_pow = C->wd_thpow;
+          line_search<false>(th, ph, gphi, T(0.5) * ap, ap, a_min, th_pow, 1);
+        }
+      } else {
+        line_search<false>(th, ph, gphi, ap, ap, a_min, th_pow, 0);
+      }
       MR_T1(3);
 #if MR_PHASE_CYCLES
       cyc[4] += res_ntr;
       cyc[5] += res_nsoc;
 #endif
       const T alpha = res_alpha;
-      const bool accepted = res_flags & 1, ftype = res_flags & 2, rej_filter = res_flags & 4;
+      const bool accepted = (res_flags & 1) && !take_anyway, ftype = res_flags & 2, rej_filter = res_flags & 4;
       const int nls = res_nls;
-      // after MR_LS_FAIL_MAX consecutive iterations without an acceptable step the solve stops with
-      // status failed (IPOPT's "restoration failed" outcome) instead of spinning to max_iter
-      ls_fail = accepted ? 0 : ls_fail + 1;
+      // no acceptable step at an infeasible point: the restoration phase (from the next iteration on)
+      if (!accepted && !take_anyway && pr_max > P.tol) {
+        resto_enter(th, ph);
+        mu_prev = mu;
+        cw()->in_wd = 0;
+        cw()->wd_short = 0;
+        acc_count = 0;
+        if (trace && ln == 0 && it < trace_cap - 2) {
+          double* tr = trace + 8 * it;
+          tr[0] = (double)kkt; tr[1] = (double)mu; tr[2] = 0.0; tr[3] = 0.0;
+          tr[4] = (double)delta; tr[5] = (double)th; tr[6] = (double)ph; tr[7] = -300.0;
+        }
+        continue;
+      }
+      // no acceptable step at a point feasible to the tolerance: the shortest tried step (the line
+      // search's fallback point); after MR_LS_FAIL_MAX such iterations in a row the solve stops
+      ls_fail = (accepted || take_anyway) ? 0 : ls_fail + 1;
       if (ls_fail >= MR_LS_FAIL_MAX) { out.status = 3; break; }
+      if (!take_anyway) cw()->wd_short = (accepted && alpha < ap) ? cw()->wd_short + 1 : 0;
 #if MR_FILTER_RESET_TRIGGER > 0
       if (filt_resets < MR_MAX_FILTER_RESETS) {
         filt_rej_iters = rej_filter ? filt_rej_iters + 1 : 0;
@@ -1245,11 +1781,12 @@ struct WaveSolver {
         }
       }
 #endif
-      if (!ftype) filter_add((T(1) - g_th) * th, ph - g_ph * th);
+      if (!(ftype && accepted) && !take_anyway) filter_add((T(1) - g_th) * th, ph - g_ph * th);
       if (trace && ln == 0 && it < trace_cap - 2) {
         double* tr = trace + 8 * it;
         tr[0] = (double)kkt; tr[1] = (double)mu; tr[2] = (double)alpha; tr[3] = (double)ad;
-        tr[4] = (double)delta; tr[5] = (double)th; tr[6] = (double)ph; tr[7] = (double)(accepted ? nls : -1);
+        tr[4] = (double)delta; tr[5] = (double)th; tr[6] = (double)ph;
+        tr[7] = (double)(take_anyway ? -100 - cw()->wd_trial : (accepted ? nls : -1));
       }
       alpha_p = alpha;
       alpha_d = ad;

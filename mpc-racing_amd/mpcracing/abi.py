@@ -10,7 +10,7 @@ HOST_TWIN_LIB = os.path.join(CSRC, "libmpcracing_host.so")
 ABI_VERSION = 101  # MR_ABI_VERSION of include/mpcracing.h
 MR_MODEL = {"kin": 0, "dyn": 1, "blend": 2, "blend_pacejka": 3, "dyn_pacejka": 4}
 MR_PREC = {"fp64": 0, "fp32": 1}
-STATUS = {0: "solved", 1: "acceptable", 2: "max_iter", 3: "failed", 4: "lane_infeasible"}
+STATUS = {0: "solved", 1: "acceptable", 2: "max_iter", 3: "failed", 4: "infeasible"}
 
 _I32 = ctypes.c_int32
 _D = ctypes.c_double
@@ -21,7 +21,7 @@ _PI32 = ctypes.POINTER(ctypes.c_int32)
 class MRConfig(ctypes.Structure):
     _fields_ = [(n, _I32) for n in ("N", "model", "precision", "lane_bounds", "max_batch", "device",
                                     "max_iter", "acceptable_iter")] + \
-               [(n, _D) for n in ("Ts", "tol", "acceptable_tol", "lane_penalty",
+               [(n, _D) for n in ("Ts", "tol", "acceptable_tol",
                                   "lambda_s", "alpha_L", "min_steer", "max_steer", "min_throttle",
                                   "max_steer_delta", "min_steer_delta", "max_throttle_delta",
                                   "min_throttle_delta", "q_v_max", "v_max", "min_s_delta",

@@ -130,5 +130,6 @@ def solver_for_config(name, max_batch, device=0, **kw):
     from .workload import CONFIGS, tyre_coeffs
     c = CONFIGS[name]
     tyres = tyre_coeffs(c["tyres"]) if c["tyres"] else None
-    return BatchSolver(c["N"], c["model"], c["precision"], c["lane"], c["Ts"], max_batch=max_batch,
+    precision = kw.pop("precision", c["precision"])
+    return BatchSolver(c["N"], c["model"], precision, c["lane"], c["Ts"], max_batch=max_batch,
                        device=device, tyres=tyres, **kw)

@@ -45,7 +45,7 @@ def build_hip(force=False, verbose=True, out=None, flags=None):
     # solve lives near 1e-38.  fp64 (the centerline kernels, fp64 solves) keeps IEEE denormals.
     # No SLP vectorisation (-fno-slp-vectorize): the v_pk_* pairs it formed in the generated dynamics
     # code cost more register moves than they saved (eval sweep 4 975 -> 3 939 VALU instructions, its
-    # scratch spills gone).  A/B on C4: profiles/r02_flags_ab.json.
+    # scratch spills gone).  A/B on C4: profiles/r03_flags_ab.json (tools/gpu_flags_ab.sh).
     cg = flags if flags is not None else DEFAULT_FLAGS
     cmd = [HIPCC, "--offload-arch=gfx950", "-O3", *cg, "-std=c++17", "-fPIC", "-shared",
            "-Wno-unused-result", "-fno-hip-fp32-correctly-rounded-divide-sqrt", "-fgpu-approx-transcendentals",

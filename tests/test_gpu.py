@@ -20,50 +20,10 @@ pytestmark = pytest.mark.gpu
 from mpcracing import workload as wl  # noqa: E402
 from mpcracing.batch import BatchSolver, solver_for_config  # noqa: E402
 from oracle import dynamics as dyn  # noqa: E402
-from oracle.nlp import MPCProblem, solve_ipm  # noqa: E402
 
 
 def _np(out):
     return {k: v.cpu().numpy() for k, v in out.items()}
-
-
-def _parity(cfg, inst, o, i, tyres=None, parity=1e-6):
-    p = MPCProblem(inst["state0"], inst["s0"], inst["cx"], inst["cy"], inst["max_error"], N=cfg["N"], Ts=cfg["Ts"],
-                   model=cfg["model"], lane_bounds=cfg["lane"], tyres=tyres, elastic=1e5 if cfg["lane"] else None)
-    r = solve_ipm(p, tol=1e-10)
-    assert r.status == 0
-    X, U, S, eC, eL = p.unpack(r.w)
-    dU = np.abs(U - o["U"][:, :, i])
-    dU[0, -1] = 0.0
-    assert dU.max() < parity, dU.max()
-    dX = np.abs(X - o["X"][:, :, i])
-    dX[3, -1] = 0.0  # vx_N: driven only by U[0, N-1]
-    assert dX.max() < parity, dX.max()
-    assert np.abs(S - o["S"][:, i]).max() < parity
-    assert np.abs(eC - o["eC"][:, i]).max() < parity and np.abs(eL - o["eL"][:, i]).max() < parity
-    assert abs(r.obj - o["obj"][i]) <= 1e-8 * max(1.0, abs(r.obj))
-
-
-@pytest.mark.parametrize("model", ["dyn", "kin"])
-def test_config1_vs_oracle(model):
-    b = wl.make_batch("C1")
-    s = BatchSolver(20, model, "fp64", False, 0.1, max_batch=1, tol=1e-10, acceptable_iter=0)
-    o = _np(s.solve(b))
-    assert o["status"][0] == 0
-    _parity(dict(N=20, Ts=0.1, model=model, lane=False), wl.instance_dicts(b)[0], o, 0)
-
-
-@pytest.mark.parametrize("name,n", [("C2", 4), ("C4", 2), ("C3", 2), ("C5", 1)])
-def test_configs_fp64_vs_oracle(name, n):
-    cfg = wl.CONFIGS[name]
-    b = wl.make_batch(name, limit=n)
-    tyres = wl.tyre_coeffs(cfg["tyres"]) if cfg["tyres"] else None
-    s = BatchSolver(cfg["N"], cfg["model"], "fp64", cfg["lane"], cfg["Ts"], max_batch=n, tol=1e-10,
-                    acceptable_iter=0, tyres=tyres)
-    o = _np(s.solve(b))
-    for i, inst in enumerate(wl.instance_dicts(b)):
-        assert o["status"][i] == 0
-        _parity(cfg, inst, o, i, tyres=tyres)
 
 
 def test_c2_full_batch_matches_host_build():
@@ -142,9 +102,9 @@ def test_c3_full_batch_lane_rows():
     s = solver_for_config("C3", 8192)
     o = _np(s.solve(b))
     ok = o["status"] == 0
-    # ~94 % solve; the unsolved ones are unsolved by the oracle's IPM and by SLSQP too
-    # (profiles/r02_audit_C3.json)
-    assert ok.mean() >= 0.9, np.bincount(o["status"], minlength=5)
+    # hard lane rows from the reference's initial guess (S_i at top speed: far outside the lane for slow
+    # cars) need IPOPT's restoration phase; >= 98 % solve to tol 1e-8 (convergence audit)
+    assert ok.mean() >= 0.98, np.bincount(o["status"], minlength=5)
     _check_feasible(cfg, o, ok, 1e-6)
     m = b["max_error"][ok]
     assert (np.abs(o["eC"][1:, ok]) <= m + 1e-6).all()  # |e_C(S_i, X_i)| <= max_error, i >= 1

@@ -1,0 +1,68 @@
+"""GPU fp64 solves vs committed oracle solutions (tests/golden/solutions_<config>.npz).
+
+The fixtures hold config 1 (script/test_mpc.py's instance; the reference's dynamic model and the
+kinematic variant) and the first 32 instances of C2, C3 (hard lane rows), C4 and C5 solved in the build
+container by oracle.ipopt.solve_ipopt (the dense IPOPT restatement with watchdog and restoration
+phase) to a KKT tolerance of 1e-10 (generator: tests/golden/make_solution_golden.py).  The GPU solves
+the same inputs in fp64 at tol 1e-10 through the C ABI and must match every instance the oracle solved
+to 1e-6 in States, U, S_hat, e_C, e_L and to 1e-8 relative in the objective -- except U[0, N-1] and
+vx_N (U[0, N-1] reaches the cost only through exp(q_v_max (vx_N - v_max)) ~ e^-60, so only the barrier
+fixes it).  Instances where the two land on different local minima of the nonconvex NLP
+are allowed only as a small, reported minority: both must then be KKT points (status 0).  No oracle
+solve runs on the GPU box.
+"""
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+from mpcracing import workload as wl  # noqa: E402
+from mpcracing.batch import BatchSolver, solver_for_config  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _fixture(name):
+    path = os.path.join(HERE, "golden", f"solutions_{name}.npz")
+    if not os.path.exists(path):
+        pytest.skip(f"{path} not generated")
+    return dict(np.load(path))
+
+
+@pytest.mark.parametrize("name", ["C1dyn", "C1kin", "C2", "C3", "C4", "C5"])
+def test_gpu_fp64_matches_oracle_solutions(name):
+    g = _fixture(name)
+    if name.startswith("C1"):  # config 1: script/test_mpc.py's inputs (N = 20, Ts = 0.1), two models
+        cfg = dict(wl.CONFIGS["C1"], model=name[2:])
+        b = wl.make_batch("C1")
+        s = BatchSolver(20, cfg["model"], "fp64", False, 0.1, max_batch=1, tol=1e-10, acceptable_iter=0)
+    else:
+        cfg = wl.CONFIGS[name]
+        b = wl.make_batch(name, limit=g["status"].size)
+        s = solver_for_config(name, b["s0"].shape[0], precision="fp64", tol=1e-10, acceptable_iter=0)
+    for k, v in b.items():  # the fixture's inputs are this config's deterministic batch
+        if v is not None:
+            assert np.array_equal(v, g["in_" + k]), k
+    o = {k: v.cpu().numpy() for k, v in s.solve(b).items()}
+    N = cfg["N"]
+    ok = g["status"] == 0
+    assert ok.mean() >= 0.9, g["status"]
+    if name == "C1dyn":  # the wrap-around rate row of MPC.py:142-143 is active there: U1_0 - U1_{N-1} = 0.2
+        assert abs((o["U"][1, 0, 0] - o["U"][1, -1, 0]) - 0.2) < 1e-6
+    same, other = [], []
+    for i in np.nonzero(ok)[0]:
+        assert o["status"][i] == 0, (i, o["status"][i])
+        dU = np.abs(g["U"][..., i] - o["U"][..., i])
+        dU[0, N - 1] = 0.0
+        dX = np.abs(g["X"][..., i] - o["X"][..., i])
+        dX[3, N] = 0.0
+        d = max(dU.max(), dX.max(), np.abs(g["S"][:, i] - o["S"][:, i]).max(),
+                np.abs(g["eC"][:, i] - o["eC"][:, i]).max(), np.abs(g["eL"][:, i] - o["eL"][:, i]).max())
+        rel = abs(g["obj"][i] - o["obj"][i]) / max(1.0, abs(g["obj"][i]))
+        (same if (d < 1e-6 and rel < 1e-8) else other).append((int(i), float(d), float(rel)))
+    print(f"{name}: {len(same)} of {int(ok.sum())} oracle-solved instances match to 1e-6; other local minima: {other}")
+    assert len(other) <= max(1, int(0.1 * ok.sum())), other

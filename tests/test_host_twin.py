@@ -110,7 +110,7 @@ def _compare(name, n, tol=1e-10, parity=1e-6):
     for i, inst in enumerate(wl.instance_dicts(b)):
         p = MPCProblem(inst["state0"], inst["s0"], inst["cx"], inst["cy"], inst["max_error"], N=cfg["N"],
                        Ts=cfg["Ts"], model=cfg["model"], lane_bounds=cfg["lane"], tyres=tyres,
-                       elastic=1e5 if cfg["lane"] else None)
+                       )
         r = solve_ipm(p, tol=1e-10)
         assert r.status == 0
         X, U, S, eC, eL = p.unpack(r.w)

@@ -52,3 +52,19 @@ def test_single_rank_is_rank0_of_eight():
         assert np.array_equal(a[k], b[k])
     with pytest.raises(ValueError):
         wl.make_batch("C4", rank=0, world=128, per_gpu=1024)  # more ranks than shards
+
+
+def test_bench_world2_real_path_with_gloo():
+    """bench.py's own world > 1 branch (not --cpu-check): init_process_group (gloo via
+    MR_BENCH_BACKEND), per-rank shards of the real path, reduce_counters and the JSON line -- the solves
+    skipped (--dry-run, no GPU here).  The line must report 2 GPUs and the union of the two shards."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["MR_BENCH_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--per-gpu", "8192",
+                        "--steps", "2", "--warmup", "0", "--dry-run"], env=env, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["dry_run"] is True
+    assert line["config"]["global_batch"] == 16384 and line["config"]["parallelism"] == "dp2 (instance shards)"
+    assert line["status_hist"]["solved"] == 16384 and line["scaling"] == "weak"
