@@ -102,7 +102,7 @@ __global__ __launch_bounds__(WL, sizeof(T) == 4 ? MR_WAVES_PER_SIMD_F32 : MR_WAV
   const int i = order ? order[blockIdx.x] : (int)blockIdx.x;
   const int64_t t_start = out.timeline ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
   Wv w{(int)threadIdx.x};
-  MR_GLOBAL T* wsi = (MR_GLOBAL T*)(ws + (int64_t)i * WS_WORDS);
+  MR_GLOBAL T* wsi = (MR_GLOBAL T*)(ws + (int64_t)i * ws_words<T>());
   // problem constants: the handle's device copy, read through the constant address space (scalar
   // loads, SGPRs); instance constants in LDS (every lane writes the same values)
   const MR_CONST ProbParams<T>& P = *(const MR_CONST ProbParams<T>*)Pdev;
@@ -187,7 +187,7 @@ __global__ __launch_bounds__(kOrderThreads) void mr_order_kernel(const double* s
 }
 
 static size_t ws_bytes_per_instance(const mr_config& c) {
-  return (size_t)WS_WORDS * (c.precision == MR_PREC_FP32 ? sizeof(float) : sizeof(double));
+  return c.precision == MR_PREC_FP32 ? (size_t)ws_words<float>() * sizeof(float) : (size_t)ws_words<double>() * sizeof(double);
 }
 
 // The handle's problem constants to its device buffer (mr_create, mr_set_tyres): the kernels read them

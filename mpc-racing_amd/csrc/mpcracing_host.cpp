@@ -42,7 +42,7 @@ static void run(const mr_config& c, const TyreCoef<double>& tf, const TyreCoef<d
 #pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
   for (int i = 0; i < B; ++i) {
     // poisoned workspace / LDS: any read-before-write shows up as NaN (device memory is not zeroed)
-    std::vector<T> ws((size_t)WS_WORDS, (T)NAN), lds((size_t)LDS_WORDS, (T)NAN);
+    std::vector<T> ws((size_t)ws_words<T>(), (T)NAN), lds((size_t)LDS_WORDS, (T)NAN);
     Job<T, MODEL> job{&P, &in, &out, (int64_t)B, (int64_t)i, ws.data(), lds.data()};
     HostWave* hw = new HostWave();
     host_wave_run(*hw, &wave_body<T, MODEL>, &job);

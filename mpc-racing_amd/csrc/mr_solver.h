@@ -43,11 +43,11 @@ constexpr int NP = NX * (NX + 1) / 2;  // packed P
 struct WF {
   enum {
     Z0 = 0, Z1 = Z0 + NZS, DZ = Z1 + NZS, S0 = DZ + NZS, S1 = S0 + NI, LAM = S1 + NI, DLAM = LAM + NI,
-    DS = DLAM + NI, NUv = DS + NI, DNU = NUv + NX, H = DNU + NX, G0 = H + NH, G1 = G0 + NZ, GL = G1 + NZ,
+    DS = DLAM + NI, DNU = DS + NI, H = DNU + NX, G0 = H + NH, G1 = G0 + NZ, GL = G1 + NZ,
     J = GL + NZ, C = J + 48, P = C + NX, PV0 = P + NP, PV1 = PV0 + NX, K = PV1 + NX, K0 = K + NU * NX,
     K1 = K0 + NU,
     // watchdog snapshot: the iterate and the search direction where the watchdog started
-    WZ = K1 + NU, WSL = WZ + NZS, WLAM = WSL + NI, WNU = WLAM + NI, WDZ = WNU + NX, WDS = WDZ + NZS,
+    WZ = K1 + NU, WSL = WZ + NZS, WLAM = WSL + NI, WDZ = WLAM + NI, WDS = WDZ + NZS,
     WDLAM = WDS + NI, WDNU = WDLAM + NI,
     // restoration phase: row relaxations p, n, their bound duals and steps, the reference point z_R
     RP = WDNU + NX, RN = RP + NI, RVP = RN + NI, RVN = RVP + NI, RDP = RVN + NI, RDN = RDP + NI, RDVP = RDN + NI,
@@ -427,29 +427,29 @@ MR_HD void apply_B(const T* J, int k, const T* w, T* y) {
   y[9] = (k == 0) ? w[0] : T(0);
   y[10] = (k == 0) ? w[1] : T(0);
 }
-// y = A^T v (11)
-template <typename T>
-MR_HD void apply_At(const T* J, int k, const T* v, T* y) {
+// y = A^T v (11); v, y may be of a wider type V than the Jacobian (fp64 multipliers of an fp32 solve)
+template <typename T, typename V>
+MR_HD void apply_At(const T* J, int k, const V* v, V* y) {
   #pragma unroll
   for (int j = 0; j < 6; ++j) {
-    T acc = T(0);
+    V acc = V(0);
     #pragma unroll
-    for (int i = 0; i < 6; ++i) acc += J[i * 8 + j] * v[i];
+    for (int i = 0; i < 6; ++i) acc += V(J[i * 8 + j]) * v[i];
     y[j] = acc;
   }
   y[6] = v[6];
-  y[7] = T(0);
-  y[8] = T(0);
-  y[9] = (k == 0) ? T(0) : v[9];
-  y[10] = (k == 0) ? T(0) : v[10];
+  y[7] = V(0);
+  y[8] = V(0);
+  y[9] = (k == 0) ? V(0) : v[9];
+  y[10] = (k == 0) ? V(0) : v[10];
 }
 // y = B^T v (3)
-template <typename T>
-MR_HD void apply_Bt(const T* J, int k, const T* v, T* y) {
-  T a0 = v[7], a1 = v[8];
+template <typename T, typename V>
+MR_HD void apply_Bt(const T* J, int k, const V* v, V* y) {
+  V a0 = v[7], a1 = v[8];
   if (k == 0) { a0 += v[9]; a1 += v[10]; }
   #pragma unroll
-  for (int i = 0; i < 6; ++i) { a0 += J[i * 8 + 6] * v[i]; a1 += J[i * 8 + 7] * v[i]; }
+  for (int i = 0; i < 6; ++i) { a0 += V(J[i * 8 + 6]) * v[i]; a1 += V(J[i * 8 + 7]) * v[i]; }
   y[0] = a0; y[1] = a1; y[2] = v[6];
 }
 
@@ -655,6 +655,9 @@ struct Solver {
   T tho_acc, pho_acc;  // original theta / barrier objective of the last trial point (restoration)
   double* trace = nullptr;  // optional per-iteration record (diagnostics)
   int trace_cap = 0;
+  // the dynamics rows' multipliers nu_k (x_k = F(x_{k-1}, u_{k-1}), k >= 1) and their watchdog copy, fp64
+  // in both precisions (correction form: eval_sweep)
+  double nub[64][NX], wnub[64][NX];
 
   MR_HD Solver(const ProbParams<T>& P_, const Inst<T>& I_, WS<T> W_) : P(P_), I(I_), W(W_), N(P_.N) {}
 
@@ -747,7 +750,7 @@ struct Solver {
         W(k, WF::DLAM + j) = T(0);
         if (act[j]) th += mr_abs(d[j] - s);
       }
-      for (int i = 0; i < NX; ++i) { W(k, WF::NUv + i) = T(0); W(k, WF::DNU + i) = T(0); }
+      for (int i = 0; i < NX; ++i) { nub[k][i] = 0.0; W(k, WF::DNU + i) = T(0); }
     }
     mu = T(0.1);
     delta_last = T(0);
@@ -768,17 +771,17 @@ struct Solver {
     nu1 = lam1 = fval = logs = T(0);
     me = NX * (N + 1);
     mi = 0;
-    T z[NZS], znext[NZS], nuk[NX], nun[NX];
+    T z[NZS], znext[NZS], nun[NX];
     load_z(0, cur, z);
-    for (int i = 0; i < NX; ++i) nuk[i] = T(0);
     for (int k = 0; k <= N; ++k) {
-      // multipliers of x_{k+1} = F(x_k, u_k): lazy update nu += alpha_p * dnu
+      // multipliers of x_{k+1} = F(x_k, u_k): lazy update nu += alpha_p * dnu (fp64), T copies for the
+      // Hessian weights
       if (k < N) {
         for (int i = 0; i < NX; ++i) {
-          T v = W(k + 1, WF::NUv + i) + alpha_p * W(k + 1, WF::DNU + i);
-          W(k + 1, WF::NUv + i) = v;
-          nun[i] = v;
-          nu1 += mr_abs(v);
+          const double v = nub[k + 1][i] + (double)alpha_p * (double)W(k + 1, WF::DNU + i);
+          nub[k + 1][i] = v;
+          nun[i] = T(v);
+          nu1 += mr_abs(nun[i]);
         }
         load_z(k + 1, cur, znext);
 #ifdef MR_DEBUG_PRINT
@@ -788,8 +791,9 @@ struct Solver {
 #endif
       }
       T H[NH], g0[NZ], g1[NZ], gl[NZ], st[NZ];
+      double dd[NZ];
       for (int i = 0; i < NH; ++i) H[i] = T(0);
-      for (int i = 0; i < NZ; ++i) { g0[i] = g1[i] = gl[i] = st[i] = T(0); }
+      for (int i = 0; i < NZ; ++i) { g0[i] = g1[i] = gl[i] = st[i] = T(0); dd[i] = 0.0; }
       if (k < N) {
         T Hd[36], J[48], fx[6];
         Dyn<T, MODEL>::fjh(P, z, z + NX, nun, fx, J, Hd);
@@ -819,7 +823,8 @@ struct Solver {
             c[i] += n - p;
             const T ip = p / vp, in = n / vn, sw = T(1) / (ip + in);
             W(k, WF::CSW + i) = sw;
-            W(k, WF::CGW0 + i) = sw * rho * (in - ip);
+            // + nu_{k+1}: the Riccati right-hand side is in correction form (below), the disturbance's is not
+            W(k, WF::CGW0 + i) = sw * rho * (in - ip) + nun[i];
             W(k, WF::CGW1 + i) = sw * (T(1) / vp - T(1) / vn);
             slam_max = mr_max(slam_max, mr_max(p * vp, n * vn));
             slam_min = mr_min(slam_min, mr_min(p * vp, n * vn));
@@ -836,13 +841,17 @@ struct Solver {
           theta += mr_abs(c[i]);
         }
         for (int i = 0; i < 48; ++i) W(k, WF::J + i) = J[i];
-        // A^T nu_{k+1}, B^T nu_{k+1} into the stationarity residual
-        T at[NX], bt[NU];
-        apply_At(J, k, nun, at);
-        apply_Bt(J, k, nun, bt);
-        for (int i = 0; i < NX; ++i) st[i] += at[i];
-        for (int i = 0; i < NU; ++i) st[NX + i] += bt[i];
+        // the dynamics rows' terms of the Lagrangian gradient, dd = [A^T nu_{k+1} - nu_k ; B^T nu_{k+1}],
+        // in fp64.  Correction form: the Riccati right-hand side is g0 + dd, so the sweeps solve for the
+        // multiplier step dnu directly (forward: dnu = P dx + p); g0 + dd and the stationarity residual are
+        // small near a solution and keep full relative precision.  (In fp32 the absolute form, nu_new =
+        // P dx + p with p ~ nu ~ 1e3, cannot resolve the stationarity below the fp32 ulp of the costates,
+        // 1.2e-4 at 1e3, above a 1e-4 tolerance.)
+        apply_At(J, k, nub[k + 1], dd);
+        apply_Bt(J, k, nub[k + 1], dd + NX);
       }
+      if (k >= 1)
+        for (int i = 0; i < NX; ++i) dd[i] -= nub[k][i];
       // cost: the scaled objective, or the restoration phase's proximity term
       Err<T> e;
       errors(I, z[0], z[1], z[6], e, true);
@@ -854,8 +863,6 @@ struct Solver {
         fval += stage_cost(P, I, k, z, e, sc, gl, H);
       }
       for (int i = 0; i < NZ; ++i) { g0[i] += gl[i]; st[i] += gl[i]; }
-      // -nu_k on the state part (k >= 1)
-      if (k >= 1) for (int i = 0; i < NX; ++i) st[i] -= nuk[i];
       // inequality rows: lazy dual update, barrier terms
       T d[NI];
       int act[NI];
@@ -943,15 +950,19 @@ struct Solver {
         }
       }
       // stationarity: x-part for k >= 1, u-part for k < N
-      if (k >= 1) for (int i = 0; i < NX; ++i) stat_max = mr_max(stat_max, mr_abs(st[i]));
-      if (k < N) for (int i = NX; i < NZ; ++i) stat_max = mr_max(stat_max, mr_abs(st[i]));
-      for (int i = 0; i < NH; ++i) W(k, WF::H + i) = H[i];
-      for (int i = 0; i < NZ; ++i) { W(k, WF::G0 + i) = g0[i]; W(k, WF::G1 + i) = g1[i]; W(k, WF::GL + i) = gl[i]; }
-      // advance
-      if (k < N) {
-        for (int i = 0; i < NZS; ++i) z[i] = znext[i];
-        for (int i = 0; i < NX; ++i) nuk[i] = nun[i];
+      for (int i = 0; i < NZ; ++i) {
+        const T sti = T((double)st[i] + dd[i]);
+        if (i < NX ? k >= 1 : k < N) stat_max = mr_max(stat_max, mr_abs(sti));
       }
+      for (int i = 0; i < NH; ++i) W(k, WF::H + i) = H[i];
+      for (int i = 0; i < NZ; ++i) {
+        W(k, WF::G0 + i) = T((double)g0[i] + dd[i]);
+        W(k, WF::G1 + i) = g1[i];
+        W(k, WF::GL + i) = gl[i];
+      }
+      // advance
+      if (k < N)
+        for (int i = 0; i < NZS; ++i) z[i] = znext[i];
     }
   }
 
@@ -1193,11 +1204,11 @@ struct Solver {
             if (dvn < T(0)) ad = mr_min(ad, -tau * vn / dvn);
           }
         }
-        // costate nu_{k+1} = P_{k+1} dx_{k+1} + p_{k+1}
+        // multiplier step dnu_{k+1} = P_{k+1} dx_{k+1} + p_{k+1} (correction form, eval_sweep)
         for (int i = 0; i < NX; ++i) {
           T v = W(k + 1, WF::PV0 + i) + mu * W(k + 1, WF::PV1 + i);
           for (int l = 0; l < NX; ++l) v += W(k + 1, WF::P + pidx(i, l)) * dx[l];
-          W(k + 1, WF::DNU + i) = v - W(k + 1, WF::NUv + i);
+          W(k + 1, WF::DNU + i) = v;  // correction form: the multiplier step itself
         }
       }
     }
@@ -1371,7 +1382,7 @@ struct Solver {
         W(k, WF::WSL + j) = W(k, sf(cur) + j); W(k, WF::WLAM + j) = W(k, WF::LAM + j);
         W(k, WF::WDS + j) = W(k, WF::DS + j); W(k, WF::WDLAM + j) = W(k, WF::DLAM + j);
       }
-      for (int i = 0; i < NX; ++i) { W(k, WF::WNU + i) = W(k, WF::NUv + i); W(k, WF::WDNU + i) = W(k, WF::DNU + i); }
+      for (int i = 0; i < NX; ++i) { wnub[k][i] = nub[k][i]; W(k, WF::WDNU + i) = W(k, WF::DNU + i); }
     }
   }
   MR_HD void wd_restore() {
@@ -1381,7 +1392,7 @@ struct Solver {
         W(k, sf(cur) + j) = W(k, WF::WSL + j); W(k, WF::LAM + j) = W(k, WF::WLAM + j);
         W(k, WF::DS + j) = W(k, WF::WDS + j); W(k, WF::DLAM + j) = W(k, WF::WDLAM + j);
       }
-      for (int i = 0; i < NX; ++i) { W(k, WF::NUv + i) = W(k, WF::WNU + i); W(k, WF::DNU + i) = W(k, WF::WDNU + i); }
+      for (int i = 0; i < NX; ++i) { nub[k][i] = wnub[k][i]; W(k, WF::DNU + i) = W(k, WF::WDNU + i); }
     }
   }
 
@@ -1440,7 +1451,7 @@ struct Solver {
           if (MR_RESTO_LAMINIT == 2) W(k, WF::LAM + j) = mu_r / W(k, sf(cur) + j);
         }
       }
-      for (int i = 0; i < NX; ++i) { W(k, WF::NUv + i) = T(0); W(k, WF::DNU + i) = T(0); }
+      for (int i = 0; i < NX; ++i) { nub[k][i] = 0.0; W(k, WF::DNU + i) = T(0); }
       if (k < N)
         for (int i = 0; i < 6; ++i) {  // the vehicle rows start satisfied too (p - n = F - x')
           T p, n;
@@ -1481,7 +1492,7 @@ struct Solver {
         W(k, WF::LAM + j) = W(k, WF::LAM + j) == T(0) ? T(0) : ln;  // inactive slots stay 0
         W(k, WF::DLAM + j) = T(0);
       }
-      for (int i = 0; i < NX; ++i) { W(k, WF::NUv + i) = T(0); W(k, WF::DNU + i) = T(0); }
+      for (int i = 0; i < NX; ++i) { nub[k][i] = 0.0; W(k, WF::DNU + i) = T(0); }
     }
     alpha_p = alpha_d = T(0);
     mu = mu_o;

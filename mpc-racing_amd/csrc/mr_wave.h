@@ -13,10 +13,12 @@
 //     products P*[A B] and [A B]^T*(P*[A B]) exchange rows through ~3 KB of LDS;
 //   * the forward substitution (sequential, 11+3 values) runs wave-uniform.
 //
-// Working set per instance (global workspace, base + i * WS_WORDS):
+// Working set per instance (global workspace, base + i * ws_words<T>()):
 //   ss[f][64]   per-stage iterate / step fields, lane-contiguous (coalesced per field); the fp32
 //               product kernel keeps them in LDS instead (SSL)
 //   rc[k][336]  per-stage Riccati record (stage Hessian, Jacobian, gradients, P, K)
+//   cold[f][64] watchdog / restoration fields (CSF)
+//   nu[2][11][64] the dynamics rows' multipliers and their watchdog copy, fp64 in both precisions
 #pragma once
 #include <new>
 
@@ -76,7 +78,7 @@ namespace mr {
 struct SSF {
   enum {
     Z0 = 0, Z1 = Z0 + NZS, DZ = Z1 + NZS, S0 = DZ + NZS, S1 = S0 + NI, LAM = S1 + NI, DLAM = LAM + NI,
-    DS = DLAM + NI, NU = DS + NI, DNU = NU + NX, GL = DNU + NX, NF = GL + NZ
+    DS = DLAM + NI, DNU = DS + NI, GL = DNU + NX, NF = GL + NZ
   };
 };
 // Stage record (stage-major, RC_STRIDE words per stage): the evaluation sweep's stage QP data
@@ -99,7 +101,7 @@ static_assert(RCF::NF <= RC_STRIDE, "record");
 // WF fields of mr_solver.h's scalar solver.
 struct CSF {
   enum {
-    WZ = 0, WSL = WZ + NZS, WLAM = WSL + NI, WNU = WLAM + NI, WDZ = WNU + NX, WDS = WDZ + NZS, WDLAM = WDS + NI,
+    WZ = 0, WSL = WZ + NZS, WLAM = WSL + NI, WDZ = WLAM + NI, WDS = WDZ + NZS, WDLAM = WDS + NI,
     WDNU = WDLAM + NI,
     RP = WDNU + NX, RN = RP + NI, RVP = RN + NI, RVN = RVP + NI, RDP = RVN + NI, RDN = RDP + NI, RDVP = RDN + NI,
     RDVN = RDVP + NI, RY = RDVN + NI, RDY = RY + NI, RZ = RDY + NI,
@@ -107,7 +109,12 @@ struct CSF {
     CDVN = CDVP + 6, CSW = CDVN + 6, CGW0 = CSW + 6, CGW1 = CGW0 + 6, NF = CGW1 + 6
   };
 };
-constexpr int64_t WS_WORDS = (int64_t)SSF::NF * WL + (int64_t)RC_STRIDE * WL + (int64_t)CSF::NF * WL;
+// The dynamics rows' multipliers nu (and their watchdog snapshot) in fp64 whatever the solve precision,
+// [2][NX][64] doubles after the cold fields: eval_sweep forms the stationarity residual and the
+// Riccati right-hand side from them in fp64 (the correction form, see there).
+constexpr int64_t WS_NU_OFF = (int64_t)SSF::NF * WL + (int64_t)RC_STRIDE * WL + (int64_t)CSF::NF * WL;  // words
+template <typename T>
+MR_HD constexpr int64_t ws_words() { return WS_NU_OFF + 2 * NX * WL * (int64_t)(sizeof(double) / sizeof(T)); }
 
 // Wave-uniform state of the watchdog and the restoration phase: one copy per wavefront next to the
 // line-search filter (LDS on the device), every lane writing the same values -- not in the per-lane
@@ -258,6 +265,10 @@ struct WaveSolver {
 
   MR_HD auto& S(int f) const { return ss[f * WL + ln]; }
   MR_HD MR_GLOBAL T& Cf(int f) const { return rc[(int64_t)RC_STRIDE * WL + f * WL + ln]; }  // cold field
+  // fp64 multiplier nu_k[i] of stage k = lane (x_k = F(x_{k-1}, u_{k-1}), k >= 1), its watchdog copy
+  MR_HD MR_GLOBAL double* nub() const { return (MR_GLOBAL double*)(rc + (int64_t)(RC_STRIDE + CSF::NF) * WL); }
+  MR_HD MR_GLOBAL double& NUd(int i) const { return nub()[i * WL + ln]; }
+  MR_HD MR_GLOBAL double& WNUd(int i) const { return nub()[(NX + i) * WL + ln]; }
   MR_HD auto& fth(int i) const { return filt[i]; }
   MR_HD auto& fph(int i) const { return filt[FMAX + i]; }
   MR_HD MR_GLOBAL T* R(int k) const { return rc + (int64_t)k * RC_STRIDE; }
@@ -349,7 +360,7 @@ struct WaveSolver {
         S(SSF::DLAM + j) = T(0);
         if (act[j]) th += mr_abs(d[j] - s);
       }
-      for (int i = 0; i < NX; ++i) { S(SSF::NU + i) = T(0); S(SSF::DNU + i) = T(0); }
+      for (int i = 0; i < NX; ++i) { NUd(i) = 0.0; S(SSF::DNU + i) = T(0); }
       MR_GLOBAL T* Rk = R(k);  // constant slots of the Riccati gather plan (frag_plan)
       Rk[RCF::CONE] = T(1);
       Rk[RCF::CZERO] = T(0);
@@ -401,15 +412,16 @@ struct WaveSolver {
     T st_l = T(0), pr_l = T(0), th_l = T(0), smax_l = T(0), smin_l = T(1e30), nu1_l = T(0), lam1_l = T(0),
       f_l = T(0), lg_l = T(0);
     int mi_l = 0;
-    // lazy multiplier update nu_k += alpha_p * dnu_k (stages 1..N)
+    // lazy multiplier update nu_k += alpha_p * dnu_k (stages 1..N), in fp64; T copies weight the
+    // dynamics Hessian
     T nuk[NX];
     for (int i = 0; i < NX; ++i) nuk[i] = T(0);
     if (own() && k >= 1) {
       for (int i = 0; i < NX; ++i) {
-        T v = S(SSF::NU + i) + alpha_p * S(SSF::DNU + i);
-        S(SSF::NU + i) = v;
-        nuk[i] = v;
-        nu1_l += mr_abs(v);
+        const double v = NUd(i) + (double)alpha_p * (double)S(SSF::DNU + i);
+        NUd(i) = v;
+        nuk[i] = T(v);
+        nu1_l += mr_abs(nuk[i]);
       }
     }
     T z[NZS];
@@ -422,16 +434,16 @@ struct WaveSolver {
 #if MR_PHASE_CYCLES
     const unsigned long long te0 = trace ? MR_CLOCK() : 0ull;
 #endif
+    // the stage record through a buffer resource: its stores do not order this sweep's later
+    // stage-field loads (different memory objects to the compiler), so those issue early
+    const WBuf<T> rbe(rc, (unsigned)WL * (unsigned)RC_STRIDE);
+    const unsigned Rk = (unsigned)k * (unsigned)RC_STRIDE;
+    T H[NH], g0[NZ], g1[NZ], gl[NZ], st[NZ], J[48];
     if (own()) {
-      // the stage record through a buffer resource: its stores do not order this sweep's later
-      // stage-field loads (different memory objects to the compiler), so those issue early
-      const WBuf<T> rbe(rc, (unsigned)WL * (unsigned)RC_STRIDE);
-      const unsigned Rk = (unsigned)k * (unsigned)RC_STRIDE;
-      T H[NH], g0[NZ], g1[NZ], gl[NZ], st[NZ];
       for (int i = 0; i < NH; ++i) H[i] = T(0);
       for (int i = 0; i < NZ; ++i) { g0[i] = g1[i] = gl[i] = st[i] = T(0); }
       if (k < N) {
-        T Hd[36], J[48], fx[6];
+        T Hd[36], fx[6];
         Dyn<T, MODEL>::fjh(P, z, z + NX, nun, fx, J, Hd);
         const int map[8] = {0, 1, 2, 3, 4, 5, 11, 12};
         int q = 0;
@@ -454,7 +466,8 @@ struct WaveSolver {
             c[i] += n - p;
             const T ip = p / vp, in = n / vn, sw = T(1) / (ip + in);
             Cf(CSF::CSW + i) = sw;
-            Cf(CSF::CGW0 + i) = sw * rho * (in - ip);
+            // + nu_{k+1}: the Riccati right-hand side is in correction form (below), the disturbance's is not
+            Cf(CSF::CGW0 + i) = sw * rho * (in - ip) + nun[i];
             Cf(CSF::CGW1 + i) = sw * (T(1) / vp - T(1) / vn);
             smax_l = mr_max(smax_l, mr_max(p * vp, n * vn));
             smin_l = mr_min(smin_l, mr_min(p * vp, n * vn));
@@ -471,12 +484,26 @@ struct WaveSolver {
           th_l += mr_abs(c[i]);
         }
         for (int i = 0; i < 48; ++i) rbe.st(J[i], 0u, Rk + RCF::J + i);
-        T at[NX], bt[NU];
-        apply_At(J, k, nun, at);
-        apply_Bt(J, k, nun, bt);
-        for (int i = 0; i < NX; ++i) st[i] += at[i];
-        for (int i = 0; i < NU; ++i) st[NX + i] += bt[i];
       }
+    }
+    // The dynamics rows' terms of the Lagrangian gradient, dd = [A^T nu_{k+1} - nu_k ; B^T nu_{k+1}], in
+    // fp64 from the fp64 multipliers (nu_{k+1} from the neighbour lane, after the Hessian so the fp64
+    // copies are not live across it).  Correction form: the Riccati right-hand side is g0 + dd, so the
+    // sweeps solve for the multipliers' step dnu directly (forward: dnu = P dx + p), and g0 + dd and the
+    // stationarity residual are small near a solution and carry full relative precision.  In fp32 the
+    // absolute form (nu_new = P dx + p with p ~ nu ~ 1e3) cannot resolve the stationarity below the
+    // fp32 ulp of the costates (1.2e-4 at 1e3), above a 1e-4 tolerance.
+    double nnd[NX];
+    for (int i = 0; i < NX; ++i) nnd[i] = wshfl(w, (own() && k >= 1) ? NUd(i) : 0.0, nxt());
+    if (own()) {
+      double dd[NZ];
+      for (int i = 0; i < NZ; ++i) dd[i] = 0.0;
+      if (k < N) {
+        apply_At(J, k, nnd, dd);
+        apply_Bt(J, k, nnd, dd + NX);
+      }
+      if (k >= 1)
+        for (int i = 0; i < NX; ++i) dd[i] -= NUd(i);
       Err<T> e;
       errors(I, z[0], z[1], z[6], e, true);
       if constexpr (RESTO) {
@@ -487,8 +514,6 @@ struct WaveSolver {
         f_l += stage_cost(P, I, k, z, e, sc, gl, H);
       }
       for (int i = 0; i < NZ; ++i) { g0[i] += gl[i]; st[i] += gl[i]; S(SSF::GL + i) = gl[i]; }
-      if (k >= 1)
-        for (int i = 0; i < NX; ++i) st[i] -= nuk[i];
       T d[NI];
       int act[NI];
       row_values(k, z, e, d, act);
@@ -590,12 +615,15 @@ struct WaveSolver {
             H[hidx(id3[a], id3[bb])] += (sig0 + sig1) * e.gC[a] * e.gC[bb] - lamdiff * e.hC[q];
         }
       }
-      if (k >= 1)
-        for (int i = 0; i < NX; ++i) st_l = mr_max(st_l, mr_abs(st[i]));
-      if (k < N)
-        for (int i = NX; i < NZ; ++i) st_l = mr_max(st_l, mr_abs(st[i]));
+      for (int i = 0; i < NZ; ++i) {
+        const T sti = T((double)st[i] + dd[i]);
+        if (i < NX ? k >= 1 : k < N) st_l = mr_max(st_l, mr_abs(sti));
+      }
       for (int i = 0; i < NH; ++i) rbe.st(H[i], 0u, Rk + RCF::H + i);
-      for (int i = 0; i < NZ; ++i) { rbe.st(g0[i], 0u, Rk + RCF::G0 + i); rbe.st(g1[i], 0u, Rk + RCF::G1 + i); }
+      for (int i = 0; i < NZ; ++i) {
+        rbe.st(T((double)g0[i] + dd[i]), 0u, Rk + RCF::G0 + i);
+        rbe.st(g1[i], 0u, Rk + RCF::G1 + i);
+      }
     }
 #if MR_PHASE_CYCLES
     const unsigned long long te1 = trace ? MR_CLOCK() : 0ull;
@@ -911,7 +939,7 @@ struct WaveSolver {
       const int N = wu(this->w, this->N), ln = this->ln;  // N wave-uniform: the stage offsets are soffsets
       const Wv w = this->w;
       // the instance's workspace (stage fields, then the records) as one wave-uniform buffer
-      const WBuf<T> wb(rc - (int64_t)SSF::NF * WL, (unsigned)WS_WORDS);
+      const WBuf<T> wb(rc - (int64_t)SSF::NF * WL, (unsigned)WS_NU_OFF);
       auto R = [](int k) { return (unsigned)(SSF::NF * WL) + (unsigned)k * (unsigned)RC_STRIDE; };
       MR_LDS T* const LDX = lds + LDX_OFF;
       // One recursion step per stage k = 0..N with three lane groups sharing the same dot product
@@ -934,11 +962,6 @@ struct WaveSolver {
       for (int a = 0; a < NU; ++a) boff[a] = ehat_slot(r0, NX + a, g0r);
       c0off = g0r ? ehat_slot(r0, 14, true) : (g1r ? RCF::PV0 + r : (g2r ? RCF::K0 + r : RCF::CZERO));
       c1off = g1r ? RCF::PV1 + r : (g2r ? RCF::K1 + r : RCF::CZERO);
-      const unsigned nuoff = (unsigned)(SSF::NU + (g1r ? r : 0)) * WL;
-      auto nu_ld = [&](int kk) -> T {
-        if constexpr (SSL) return ss[nuoff + kk];
-        else return wb.ld((unsigned)kk, nuoff);
-      };
       static_assert(3 * WL <= LP_OFF + 16 * LDS_LD, "du staging");
       // LDS target of each lane's step result (branch-free, one store): group 0 dx_{k+1}[r] at
       // LDX[(k + 1) 12 + r] (row N + 1 <= 64; N = 63: the discard slots), group 2 du_k[r] at
@@ -951,7 +974,7 @@ struct WaveSolver {
       // with one exit test per step at its end (uniform control, no copies of in-flight loads): the
       // waits for a set are exact vmcnt counts, not drains at the loop head.
       struct FwdRow {
-        T rw[NX], bw[NU], c0, c1, nu;
+        T rw[NX], bw[NU], c0, c1;
       };
       auto fload = [&](int kk, FwdRow& f) {
         kk = kk < N ? kk : N;
@@ -962,7 +985,6 @@ struct WaveSolver {
         for (int a = 0; a < NU; ++a) f.bw[a] = wb.ld(ro, (unsigned)boff[a]);
         f.c0 = wb.ld(ro, (unsigned)c0off);
         f.c1 = wb.ld(ro, (unsigned)c1off);
-        f.nu = nu_ld(wu(w, kk));
       };
       auto fstep = [&](int k, const FwdRow& f) {
         T dxv[NX];
@@ -990,9 +1012,9 @@ struct WaveSolver {
         lds[lbase + lstep * k] = g0r ? accx : acc;
         const bool dn = g1r & (k >= 1);
         if constexpr (SSL) {
-          if (dn) ss[(SSF::DNU + r) * WL + k] = acc - f.nu;
+          if (dn) ss[(SSF::DNU + r) * WL + k] = acc;
         } else {  // branch-free: other lanes write stage k's record discard slot
-          wb.st(acc - f.nu, (unsigned)k, dn ? (unsigned)(SSF::DNU + r) * WL : R(k) + RCF::JUNK - (unsigned)k);
+          wb.st(acc, (unsigned)k, dn ? (unsigned)(SSF::DNU + r) * WL : R(k) + RCF::JUNK - (unsigned)k);
         }
       };
       FwdRow fa, fb, fc;
@@ -1116,12 +1138,12 @@ struct WaveSolver {
       for (int i = 0; i < 6; ++i) dx[i] += wv[i];
       if (ln == k)
         for (int i = 0; i < 6; ++i) myw[i] = wv[i];
-      // costate nu_{k+1} = P_{k+1} dx_{k+1} + p_{k+1}
+      // multiplier step dnu_{k+1} = P_{k+1} dx_{k+1} + p_{k+1} (correction form, eval_sweep)
       if (ln == k + 1)
         for (int i = 0; i < NX; ++i) {
           T v = Rn[RCF::PV0 + i] + mu * Rn[RCF::PV1 + i];
           for (int l = 0; l < NX; ++l) v += Pn[pidx(i, l)] * dx[l];
-          S(SSF::DNU + i) = v - S(SSF::NU + i);
+          S(SSF::DNU + i) = v;  // correction form: the multiplier step itself
         }
     }
     T ap_l = T(1), ad_l = T(1), g_l = T(0);
@@ -1460,7 +1482,7 @@ struct WaveSolver {
         Cf(CSF::WSL + j) = S(sf(cur) + j); Cf(CSF::WLAM + j) = S(SSF::LAM + j);
         Cf(CSF::WDS + j) = S(SSF::DS + j); Cf(CSF::WDLAM + j) = S(SSF::DLAM + j);
       }
-      for (int i = 0; i < NX; ++i) { Cf(CSF::WNU + i) = S(SSF::NU + i); Cf(CSF::WDNU + i) = S(SSF::DNU + i); }
+      for (int i = 0; i < NX; ++i) { WNUd(i) = NUd(i); Cf(CSF::WDNU + i) = S(SSF::DNU + i); }
     }
     wsync(w);
   }
@@ -1472,7 +1494,7 @@ struct WaveSolver {
         S(sf(cur) + j) = Cf(CSF::WSL + j); S(SSF::LAM + j) = Cf(CSF::WLAM + j);
         S(SSF::DS + j) = Cf(CSF::WDS + j); S(SSF::DLAM + j) = Cf(CSF::WDLAM + j);
       }
-      for (int i = 0; i < NX; ++i) { S(SSF::NU + i) = Cf(CSF::WNU + i); S(SSF::DNU + i) = Cf(CSF::WDNU + i); }
+      for (int i = 0; i < NX; ++i) { NUd(i) = WNUd(i); S(SSF::DNU + i) = Cf(CSF::WDNU + i); }
     }
     wsync(w);
   }
@@ -1521,7 +1543,7 @@ struct WaveSolver {
         Cf(CSF::RDY + j) = T(0);
         S(SSF::DLAM + j) = T(0);
       }
-      for (int i = 0; i < NX; ++i) { S(SSF::NU + i) = T(0); S(SSF::DNU + i) = T(0); }
+      for (int i = 0; i < NX; ++i) { NUd(i) = 0.0; S(SSF::DNU + i) = T(0); }
       if (k < N)
         for (int i = 0; i < 6; ++i) {  // the vehicle rows start satisfied too (p - n = F - x')
           T p, n;
@@ -1566,7 +1588,7 @@ struct WaveSolver {
         S(SSF::LAM + j) = lam0 == T(0) ? T(0) : lnew;  // inactive slots stay 0
         S(SSF::DLAM + j) = T(0);
       }
-      for (int i = 0; i < NX; ++i) { S(SSF::NU + i) = T(0); S(SSF::DNU + i) = T(0); }
+      for (int i = 0; i < NX; ++i) { NUd(i) = 0.0; S(SSF::DNU + i) = T(0); }
     }
     alpha_p = alpha_d = T(0);
     mu = mu_o;
@@ -1895,11 +1917,11 @@ MR_HD void write_lam_g(Solver& S, const mr_outputs& out, int64_t B, int64_t i, i
   const int rows = 13 * N + 9;
   auto put = [&](int row, double v) { out.lam_g[(int64_t)row * B + i] = v; };
   auto lam = [&](int j) { return (double)S.S(SSF::LAM + j); };
-  T nu1[NX];
-  for (int q = 0; q < NX; ++q) nu1[q] = wshfl(w, S.own() ? S.S(SSF::NU + q) : T(0), 1);
+  double nu1[NX];
+  for (int q = 0; q < NX; ++q) nu1[q] = wshfl(w, S.own() ? S.NUd(q) : 0.0, 1);
   const double ds1 = wshfl(w, S.own() && k < N ? (lam(5) - lam(4)) * isc : 0.0, 0);
   if (k >= 1 && k <= N)
-    for (int q = 0; q < 6; ++q) put(7 + 7 * (k - 1) + q, -(double)S.S(SSF::NU + q) * isc);
+    for (int q = 0; q < 6; ++q) put(7 + 7 * (k - 1) + q, -S.NUd(q) * isc);
   if (k < N) {
     put(7 + 7 * k + 6, (lam(5) - lam(4)) * isc);  // Delta-S row of i = k + 1 (u[2] box of stage k)
     const int b = 7 + 7 * N + 6 * k;
@@ -1920,10 +1942,11 @@ MR_HD void write_lam_g(Solver& S, const mr_outputs& out, int64_t B, int64_t i, i
   if (k == 0) {
     put(0, ds1);  // S_0 == s0
     MR_GLOBAL T* R0 = S.R(0);
-    T J[48], at[NX];
+    T J[48];
+    double at[NX];
     for (int q = 0; q < 48; ++q) J[q] = R0[RCF::J + q];
     apply_At(J, 0, nu1, at);
-    for (int q = 0; q < 6; ++q) put(1 + q, -(double)at[q] * isc);  // X_{q,0} == state0
+    for (int q = 0; q < 6; ++q) put(1 + q, -at[q] * isc);  // X_{q,0} == state0
     put(rows - 2, S.I.has_thr0 ? (lam(7) - lam(6)) * isc : NAN);
     put(rows - 1, S.I.has_steer0 ? (lam(9) - lam(8)) * isc : NAN);
   }

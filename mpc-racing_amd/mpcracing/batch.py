@@ -35,8 +35,8 @@ class BatchSolver:
             c.tol = float(tol)
         elif precision == "fp32":
             # the reference's own IPOPT options (control/MPC.py:152-161): tol 1e-4, acceptable_tol 1e-2,
-            # IPOPT's acceptable_iter 15 -- an fp32 solve cannot resolve a scaled KKT error much below
-            # ~1e-3, so without the acceptable exit such instances would run to max_iter
+            # IPOPT's acceptable_iter 15 (the fp32 solve resolves the KKT error to 1e-4 through its fp64
+            # multipliers, mr_wave.h eval_sweep; the acceptable exit catches the rare stalls)
             c.tol = 1e-4
             c.acceptable_tol = 1e-2
         for k, v in overrides.items():
