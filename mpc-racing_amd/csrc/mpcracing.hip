@@ -98,7 +98,7 @@ struct SSInLDS { static constexpr bool value = MR_SS_LDS && sizeof(T) == 4; };
 template <typename T, int MODEL>
 __global__ __launch_bounds__(WL, sizeof(T) == 4 ? MR_WAVES_PER_SIMD_F32 : MR_WAVES_PER_SIMD_F64) void mr_wave_kernel(const ProbParams<T>* Pdev, mr_inputs in, mr_outputs out, int B,
                                                                          T* ws, const int* order) {
-  __shared__ T lds[LDS_WORDS];
+  __shared__ alignas(16) T lds[LDS_WORDS];
   const int i = order ? order[blockIdx.x] : (int)blockIdx.x;
   const int64_t t_start = out.timeline ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
   Wv w{(int)threadIdx.x};

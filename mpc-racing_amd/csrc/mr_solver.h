@@ -543,34 +543,40 @@ MR_HD void ltsolve6(const T* L, T* b) {
     b[i] = v / L[i * 6 + i];
   }
 }
+// Evaluated in fp64 whatever T: where a relaxation is active (small sw) the vehicle block of P~ is the
+// difference of two nearly equal terms of the size of P_vv (P_vv - P_vv M^-1 P_vv -> the parallel sum of
+// P_vv and diag(sw)); in fp32 that difference is rounding noise of order eps |P_vv|, the next stages' Q_uu
+// lose definiteness and the inertia correction climbs to 1e6..1e10 (profiles/r03_resto_fp64cond.json).
+// Only restoration-phase factorisations run this.
 template <typename T>
 MR_HD bool noise_cond(T* Pm, T* p0, T* p1, const T* sw, const T* gw0, const T* gw1) {
-  T M[36], L[36];
+  typedef double D;
+  D M[36], L[36];
   for (int i = 0; i < 6; ++i)
-    for (int j = 0; j < 6; ++j) M[i * 6 + j] = Pm[pidx(i, j)] + (i == j ? sw[i] : T(0));
+    for (int j = 0; j < 6; ++j) M[i * 6 + j] = (D)Pm[pidx(i, j)] + (i == j ? (D)sw[i] : 0.0);
   if (!chol6(M, L)) return false;
-  T Y[6][NX], y0[6], y1[6];
+  D Y[6][NX], y0[6], y1[6];
   for (int j = 0; j < NX; ++j) {
-    T col[6];
-    for (int i = 0; i < 6; ++i) col[i] = Pm[pidx(i, j)];
+    D col[6];
+    for (int i = 0; i < 6; ++i) col[i] = (D)Pm[pidx(i, j)];
     lsolve6(L, col);
     for (int i = 0; i < 6; ++i) Y[i][j] = col[i];
   }
-  for (int i = 0; i < 6; ++i) { y0[i] = p0[i] + gw0[i]; y1[i] = p1[i] + gw1[i]; }
+  for (int i = 0; i < 6; ++i) { y0[i] = (D)p0[i] + (D)gw0[i]; y1[i] = (D)p1[i] + (D)gw1[i]; }
   lsolve6(L, y0);
   lsolve6(L, y1);
   for (int i = 0; i < NX; ++i) {
     for (int j = i; j < NX; ++j) {
-      T v = Pm[pidx(i, j)];
+      D v = (D)Pm[pidx(i, j)];
       for (int a = 0; a < 6; ++a) v -= Y[a][i] * Y[a][j];
-      Pm[pidx(i, j)] = v;
+      Pm[pidx(i, j)] = (T)v;
     }
   }
   for (int i = 0; i < NX; ++i) {
-    T v0 = p0[i], v1 = p1[i];
+    D v0 = (D)p0[i], v1 = (D)p1[i];
     for (int a = 0; a < 6; ++a) { v0 -= Y[a][i] * y0[a]; v1 -= Y[a][i] * y1[a]; }
-    p0[i] = v0;
-    p1[i] = v1;
+    p0[i] = (T)v0;
+    p1[i] = (T)v1;
   }
   return true;
 }

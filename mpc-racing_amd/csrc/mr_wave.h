@@ -69,6 +69,9 @@
 #ifndef MR_FWD_TREE
 #define MR_FWD_TREE 0  // 1: the forward recursion's dot products as three chains (A/B option)
 #endif
+#ifndef MR_RIC_AHEAD
+#define MR_RIC_AHEAD 2  // stages the Riccati's operand gathers run ahead of the factorisation (2 or 3)
+#endif
 #ifndef MR_PRIO_ITER
 #define MR_PRIO_ITER 0  // > 0: the wave raises its issue priority (s_setprio) at this iteration
 #endif
@@ -749,32 +752,36 @@ struct WaveSolver {
   // stage k's relaxed vehicle rows (mr_solver.h noise_cond): M = P_vv + diag(sw) = L L^T (every lane,
   // registers), Y = L^-1 [P_v. | p0_v + gw0 | p1_v + gw1] (lane c < 13: column c, to the LX scratch
   // tile), then P^ -= Y^T Y entry-wise.  False if M is not positive definite.
+  // In fp64 whatever T (mr_solver.h noise_cond: the vehicle block of P^ is otherwise fp32 rounding noise
+  // where a relaxation is active); the L^-1 columns go through the LX scratch tile as doubles.
   MR_HD bool noise_tile(int k, MR_LDS T* LP) const {
-    MR_LDS T* const LX = lds + LX_OFF;
+    typedef double D;
+    static_assert(6 * 16 * sizeof(D) <= 16 * LDS_LD * sizeof(T), "LX scratch holds 6 x 16 doubles");
+    MR_LDS D* const LX = (MR_LDS D*)(lds + LX_OFF);
     const MR_GLOBAL T* cb = rc + (int64_t)RC_STRIDE * WL;
     const int l = ln;
-    T sw[6], gw0[6], gw1[6], M[36], L[36];
+    D sw[6], gw0[6], gw1[6], M[36], L[36];
     for (int i = 0; i < 6; ++i) {
-      sw[i] = cb[(CSF::CSW + i) * WL + k];
-      gw0[i] = cb[(CSF::CGW0 + i) * WL + k];
-      gw1[i] = cb[(CSF::CGW1 + i) * WL + k];
+      sw[i] = (D)cb[(CSF::CSW + i) * WL + k];
+      gw0[i] = (D)cb[(CSF::CGW0 + i) * WL + k];
+      gw1[i] = (D)cb[(CSF::CGW1 + i) * WL + k];
     }
     for (int i = 0; i < 6; ++i)
-      for (int j = 0; j < 6; ++j) M[i * 6 + j] = LP[i * LDS_LD + j] + (i == j ? sw[i] : T(0));
+      for (int j = 0; j < 6; ++j) M[i * 6 + j] = (D)LP[i * LDS_LD + j] + (i == j ? sw[i] : 0.0);
     const bool ok = chol6(M, L);
     if (!wuni(w, ok)) return false;
     const int c = l < 13 ? l : 0;
-    T col[6];
-    for (int i = 0; i < 6; ++i) col[i] = LP[i * LDS_LD + c] + (c == 11 ? gw0[i] : (c == 12 ? gw1[i] : T(0)));
+    D col[6];
+    for (int i = 0; i < 6; ++i) col[i] = (D)LP[i * LDS_LD + c] + (c == 11 ? gw0[i] : (c == 12 ? gw1[i] : 0.0));
     lsolve6(L, col);
     if (l < 13)
       for (int a = 0; a < 6; ++a) LX[a * 16 + l] = col[a];
     wsync_lds(w);
     for (int e = l; e < NX * 13; e += WL) {
       const int i = e / 13, j = e - 13 * (e / 13);
-      T v = LP[i * LDS_LD + j];
+      D v = (D)LP[i * LDS_LD + j];
       for (int a = 0; a < 6; ++a) v -= LX[a * 16 + i] * LX[a * 16 + j];
-      LP[i * LDS_LD + j] = v;
+      LP[i * LDS_LD + j] = (T)v;
     }
     wsync_lds(w);
     return true;
@@ -806,6 +813,10 @@ struct WaveSolver {
     T raw_a[NGATHER], raw_b[NGATHER], raw_c[NGATHER];
     frag_load(rb, R(N - 1), fp, raw_a);
     frag_load(rb, R(N >= 2 ? N - 2 : 0), fp, raw_b);
+#if MR_RIC_AHEAD == 3
+    T raw_d[NGATHER];
+    frag_load(rb, R(N >= 3 ? N - 3 : 0), fp, raw_c);
+#endif
     {  // terminal cost-to-go: P_N = H_N,xx + delta I, p_N = g_N.  Branch-free (lanes >= NX write
        // discard slots), so at least as many memory ops follow the first prefetch on this path as
        // on the loop back-edge and the wait at the loop head stays exact.
@@ -837,7 +848,7 @@ struct WaveSolver {
       const unsigned Rk = (unsigned)wu(w, (int)R(k));
       T eb[4], dq[4];
       frag_finish(dd, raw_use, eb, dq);
-      frag_load(rb, (unsigned)wu(w, (int)R(k >= 2 ? k - 2 : 0)), fp, raw_fill);  // unconditional: k < 2 re-read stage 0's record
+      frag_load(rb, (unsigned)wu(w, (int)R(k >= MR_RIC_AHEAD ? k - MR_RIC_AHEAD : 0)), fp, raw_fill);  // unconditional: k < AHEAD re-read stage 0's record
       // X = P^ E^  (A fragment s: P^[c][4s+g])
       // two independent 2-MFMA accumulation chains (k = 0..7 | 8..15) instead of one 4-long
       // dependent chain: half the MFMA latency on the stage's critical path
@@ -906,6 +917,20 @@ struct WaveSolver {
     // next two, and the loop keeps one back-edge block (exact prefetch waits at the loop head).
     // Buffer roles rotate a -> c -> b -> a over the three unrolled steps.
     bool ok = true;
+#if MR_RIC_AHEAD == 3
+    // A/B option: gathers three stages ahead, four rotating buffers (a -> d -> c -> b -> a)
+    for (int k = N - 1;; k -= 4) {
+      ok = step(k, raw_a, raw_d) & ok;
+      if (k == 0) break;
+      ok = step(k - 1, raw_b, raw_a) & ok;
+      if (k == 1) break;
+      ok = step(k - 2, raw_c, raw_b) & ok;
+      if (k == 2) break;
+      ok = step(k - 3, raw_d, raw_c) & ok;
+      if (k == 3) break;
+      if (!wuni(w, ok)) return false;
+    }
+#else
     for (int k = N - 1;; k -= 3) {
       ok = step(k, raw_a, raw_c) & ok;
       if (k == 0) break;
@@ -915,6 +940,7 @@ struct WaveSolver {
       if (k == 2) break;
       if (!wuni(w, ok)) return false;
     }
+#endif
     if (!wuni(w, ok)) return false;
     wsync(w);  // records (P, p, K, k0, k1) visible to every lane
     return true;

@@ -1,12 +1,23 @@
 """Convergence audit (CPU): instances the solver does not solve, re-run by independent methods.
 
 For the first ``n`` instances of a config, the scalar C++ build of the solver (same algorithm as the
-kernel) finds the instances that end in max_iter / failed / lane-infeasible; each of those is then
-given to (a) the oracle's dense fp64 IPM (oracle/nlp.py, same IPOPT-style rules, torch autograd
-derivatives) and (b) scipy SLSQP from the reference's initial guess (an independent algorithm).  An
-instance that (a) or (b) solves to a KKT point but the product does not is a solver weakness.
+kernel, fp64, the library's fp64 defaults: scaled KKT tol 1e-8, acceptable 1e-6 over 15 iterations)
+finds the instances that end in max_iter / failed / infeasible; each of those (up to ``max_checked``)
+is then given to
+  (a) the oracle's dense restatement of IPOPT (oracle/ipopt.py: the same rules incl. the watchdog and
+      the l1 restoration phase, full-space KKT matrix, LDL inertia, torch autograd derivatives), and
+  (b) scipy SLSQP from the reference's initial guess (an independent algorithm),
+both on the hard NLP (lane rows as the reference writes them, MPC.py:135).  An instance that (a) or (b)
+solves to a KKT point but the product does not is a solver weakness; one that (b) makes feasible but the
+product calls infeasible (status 4) is a wrong label.
 
-Usage: python mpc-racing_amd/tools/convergence_audit.py C3 256 [max_checked] > profiles/r02_audit_C3.json
+For the blended models the audit also records where the product's final trajectory sits relative to
+the blend law's clip corners (speed hypot(vx, vy) at Vblendmin = 2 / Vblendmax = 15 m/s,
+models/BlendedBicycleModel.py:24-26, models/VehicleParameters.py:37-38): the dynamics are not
+differentiable there, and the interior-point iteration cycles when the optimum puts predicted speeds on
+a corner.  Reported for every unsolved instance and, for comparison, over all solved ones.
+
+Usage: python mpc-racing_amd/tools/convergence_audit.py C3 1024 [max_checked] > profiles/r03_audit_C3.json
 """
 import json
 import os
@@ -21,12 +32,23 @@ sys.path.insert(0, os.path.join(REPO, "mpc-racing_amd"))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
+V_CORNERS = (2.0, 15.0)
+
+
+def corner_stats(X):
+    """X [6][N+1]: smallest distance of the predicted speeds (stages 1..N) to a blend corner, and the
+    number of stages within 0.05 m/s of one."""
+    v = np.hypot(X[3, 1:], X[4, 1:])
+    d = np.min(np.abs(v[:, None] - np.array(V_CORNERS)[None, :]), axis=1)
+    return float(d.min()), int((d < 0.05).sum())
+
 
 def main():
     import torch
     import host_twin as ht
     from mpcracing import workload as wl
-    from oracle.nlp import MPCProblem, solve_ipm, solve_slsqp, kkt_residuals
+    from oracle.nlp import MPCProblem, solve_slsqp
+    from oracle.ipopt import solve_ipopt
     name, n = sys.argv[1], int(sys.argv[2])
     max_checked = int(sys.argv[3]) if len(sys.argv) > 3 else 20
     cfg = wl.CONFIGS[name]
@@ -36,27 +58,35 @@ def main():
                   acceptable_tol=1e-6)
     t0 = time.time()
     o = ht.solve(c, b, tyres=tyres, nthreads=len(os.sched_getaffinity(0)), scalar=True)
-    rec = {"config": name, "n": n, "status_hist": np.bincount(o["status"], minlength=5).tolist(),
+    rec = {"config": name, "n": n, "product": "scalar C++ fp64 build (mr_solver.h Solver), tol 1e-8",
+           "status_hist": np.bincount(o["status"], minlength=5).tolist(),
+           "status_names": ["solved", "acceptable", "max_iter", "failed", "infeasible"],
            "iters_mean": float(o["iters"].mean()), "cpu_s": time.time() - t0, "unsolved": []}
+    blend = cfg["model"].startswith("blend")
+    if blend:
+        ok = np.nonzero(o["status"] <= 1)[0]
+        cs = np.array([corner_stats(o["X"][:, :, i]) for i in ok])
+        rec["solved_corner"] = {"n": int(ok.size), "frac_with_stage_within_0.05": float((cs[:, 1] > 0).mean()),
+                                "median_min_dist": float(np.median(cs[:, 0]))}
     bad = np.nonzero(o["status"] >= 2)[0][:max_checked]
     insts = wl.instance_dicts(b)
     T = lambda a: torch.tensor(a, dtype=torch.float64)  # noqa: E731
     for i in bad:
         inst = insts[i]
         p = MPCProblem(inst["state0"], inst["s0"], inst["cx"], inst["cy"], inst["max_error"], N=cfg["N"],
-                       Ts=cfg["Ts"], model=cfg["model"], lane_bounds=cfg["lane"], tyres=tyres,
-                       elastic=1e5 if cfg["lane"] else None)
-        r = solve_ipm(p, tol=1e-8, max_iter=500)
+                       Ts=cfg["Ts"], model=cfg["model"], lane_bounds=cfg["lane"], tyres=tyres)
         e = {"i": int(i), "status": int(o["status"][i]), "iters": int(o["iters"][i]), "kkt": float(o["kkt"][i]),
-             "oracle_status": r.status, "oracle_iters": r.iters, "oracle_kkt": r.kkt}
+             "obj": float(o["obj"][i])}
+        if blend:
+            e["corner_min_dist"], e["corner_stages"] = corner_stats(o["X"][:, :, i])
+        t1 = time.time()
+        r = solve_ipopt(p, tol=1e-8, max_iter=500, acceptable_tol=1e-6, acceptable_iter=15)
+        e.update(oracle_status=int(r.status), oracle_iters=int(r.iters), oracle_kkt=float(r.kkt),
+                 oracle_obj=float(r.obj), oracle_s=time.time() - t1)
         s = solve_slsqp(p)
-        g = np.abs(p.g(T(s.x)).numpy()).max()
-        dmin = p.d(T(s.x)).numpy().min()
-        e.update(slsqp_status=int(s.status), slsqp_eq=float(g), slsqp_ineq=float(dmin), slsqp_obj=float(s.fun),
-                 oracle_obj=float(r.obj))
-        if cfg["lane"]:
-            t = s.x[9 * cfg["N"] + 7:]
-            e["slsqp_lane_slack_max"] = float(np.max(t))
+        w = T(s.x)
+        e.update(slsqp_status=int(s.status), slsqp_eq=float(np.abs(p.g(w).numpy()).max()),
+                 slsqp_ineq=float(p.d(w).numpy().min()), slsqp_obj=float(s.fun))
         rec["unsolved"].append(e)
         print(json.dumps(e), file=sys.stderr, flush=True)
     print(json.dumps(rec, indent=1))

@@ -54,6 +54,8 @@ def main():
     rec = {"config": name, "dispatch_order": order, "B": int(B), "makespan_ms": mk,
            "sum_instance_ms": float(dur.sum()), "slot_utilisation": float(dur.sum() / (slots * mk)),
            "ms_per_iter_batch_median": float(np.median(dur / np.maximum(it, 1))),
+           "ms_per_iter_batch_mean": float(dur.sum() / max(int(it.sum()), 1)),
+           "iters_total": int(it.sum()),
            "longest": [{"i": int(i), "iters": int(it[i]), "status": int(status[i]), "start_ms": float(st[i]),
                         "dur_ms": float(dur[i])} for i in long_[:8]],
            "longest_solo_ms": solo,
