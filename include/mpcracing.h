@@ -34,8 +34,9 @@ extern "C" {
 
 /* ABI version (mr_version()): bumped whenever a struct layout or an entry point's meaning changes, so
    a caller built against another header can refuse to run (101: mr_config.dispatch_order,
-   mr_outputs.lam_g / timeline, mr_config without lane_penalty (hard lane rows), status 4 = infeasible) */
-#define MR_ABI_VERSION 101
+   mr_outputs.lam_g / timeline, mr_config without lane_penalty (hard lane rows), status 4 = infeasible;
+   102: mr_inputs.order_hint, dispatch_order 2) */
+#define MR_ABI_VERSION 102
 
 #define MR_OK 0
 #define MR_ERR_ARG (-1)
@@ -88,7 +89,10 @@ typedef struct mr_config {
   /* workgroup dispatch order of a batch (results do not depend on it: instances are independent):
      0 = instance order; 1 = (default) a stable three-tier partition so the likely long solves start
      first: tier 0 = v >= 40 m/s, or throttle <= -0.5 at v <= 20 m/s (hard braking through a blend
-     corner of the model); tier 1 = the rest outside 16.5 < v < 39; tier 2 = the others */
+     corner of the model); tier 1 = the rest outside 16.5 < v < 39; tier 2 = the others (a cold-start
+     guess from the model's nonsmooth / stiff regions, for batches without history);
+     2 = longest-expected-first by mr_inputs.order_hint (e.g. the previous MPC tick's iters of the same
+     vehicles: LPT scheduling with a distribution-agnostic estimate; instance order when the hint is NULL) */
   int32_t dispatch_order;
 } mr_config;
 
@@ -103,6 +107,9 @@ typedef struct mr_inputs {
                             drop-in passes that value here to keep the quirk. */
   const double* u_init;  /* optional [2][N][B] initial controls (already shifted last_controls,
                             control/MPC.py:120-125); NULL -> (throttle0, steer0) repeated */
+  const int32_t* order_hint; /* optional [B] expected cost of each instance (larger = dispatched earlier),
+                            read only with mr_config.dispatch_order = 2, before the solve starts (so the
+                            previous call's mr_outputs.iters may be passed in place) */
 } mr_inputs;
 
 typedef struct mr_outputs {

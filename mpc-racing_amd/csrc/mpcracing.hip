@@ -186,6 +186,28 @@ __global__ __launch_bounds__(kOrderThreads) void mr_order_kernel(const double* s
   }
 }
 
+// dispatch_order = 2: workgroups take instances in decreasing order_hint (longest expected first), e.g.
+// the previous MPC tick's iteration counts.  One workgroup: bucket histogram (hint clamped to
+// 0..kHintBuckets-1) in LDS, a scan from the largest bucket down, then an atomic scatter (the order within
+// a bucket is arbitrary; results do not depend on the order).
+constexpr int kHintBuckets = kOrderThreads;
+__device__ __forceinline__ int hint_bucket(int h) { return h < 0 ? 0 : (h >= kHintBuckets ? kHintBuckets - 1 : h); }
+__global__ __launch_bounds__(kOrderThreads) void mr_order_hint_kernel(const int32_t* hint, int B, int* order) {
+  __shared__ int cnt[kHintBuckets];
+  __shared__ int scan[kOrderThreads];
+  const int t = threadIdx.x;
+  cnt[t] = 0;
+  __syncthreads();
+  for (int i = t; i < B; i += kOrderThreads) atomicAdd(&cnt[hint_bucket(hint[i])], 1);
+  __syncthreads();
+  const int r = kHintBuckets - 1 - t;  // thread t scans bucket r: the largest bucket first
+  const int c = cnt[r];
+  const int incl = order_scan(scan, t, c);
+  cnt[r] = incl - c;  // first slot of bucket r
+  __syncthreads();
+  for (int i = t; i < B; i += kOrderThreads) order[atomicAdd(&cnt[hint_bucket(hint[i])], 1)] = i;
+}
+
 static size_t ws_bytes_per_instance(const mr_config& c) {
   return c.precision == MR_PREC_FP32 ? (size_t)ws_words<float>() * sizeof(float) : (size_t)ws_words<double>() * sizeof(double);
 }
@@ -210,6 +232,10 @@ static int launch(mr_handle* h, int B, const mr_inputs* in, mr_outputs* out, hip
   const int* order = nullptr;
   if (h->cfg.dispatch_order == 1 && B > 1) {
     hipLaunchKernelGGL(mr_order_kernel, dim3(1), dim3(kOrderThreads), 0, st, in->state0, B, h->order);
+    HIP_TRY(hipGetLastError());
+    order = h->order;
+  } else if (h->cfg.dispatch_order == 2 && in->order_hint && B > 1) {
+    hipLaunchKernelGGL(mr_order_hint_kernel, dim3(1), dim3(kOrderThreads), 0, st, in->order_hint, B, h->order);
     HIP_TRY(hipGetLastError());
     order = h->order;
   }
@@ -434,6 +460,7 @@ int mr_create(mr_handle** out, const mr_config* cfg) {
   if (cfg->precision != MR_PREC_FP64 && cfg->precision != MR_PREC_FP32) return fail(MR_ERR_ARG, "bad precision");
   if (cfg->max_batch < 1) return fail(MR_ERR_ARG, "max_batch < 1");
   if (!(cfg->Ts > 0)) return fail(MR_ERR_ARG, "Ts must be > 0");
+  if (cfg->dispatch_order < 0 || cfg->dispatch_order > 2) return fail(MR_ERR_ARG, "dispatch_order must be 0, 1 or 2");
   {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;

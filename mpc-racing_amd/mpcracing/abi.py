@@ -7,7 +7,7 @@ CSRC = os.path.abspath(os.path.join(HERE, "..", "csrc"))
 PRODUCT_LIB = os.path.join(CSRC, "libmpcracing.so")
 HOST_TWIN_LIB = os.path.join(CSRC, "libmpcracing_host.so")
 
-ABI_VERSION = 101  # MR_ABI_VERSION of include/mpcracing.h
+ABI_VERSION = 102  # MR_ABI_VERSION of include/mpcracing.h
 MR_MODEL = {"kin": 0, "dyn": 1, "blend": 2, "blend_pacejka": 3, "dyn_pacejka": 4}
 MR_PREC = {"fp64": 0, "fp32": 1}
 STATUS = {0: "solved", 1: "acceptable", 2: "max_iter", 3: "failed", 4: "infeasible"}
@@ -31,7 +31,8 @@ class MRConfig(ctypes.Structure):
 
 
 class MRInputs(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_void_p) for n in ("state0", "s0", "cx", "cy", "max_error", "runtime", "u_init")]
+    _fields_ = [(n, ctypes.c_void_p) for n in ("state0", "s0", "cx", "cy", "max_error", "runtime", "u_init",
+                                               "order_hint")]
 
 
 class MROutputs(ctypes.Structure):

@@ -66,6 +66,10 @@ class BatchSolver:
 
     def to_device(self, batch):
         out = {}
+        h = batch.get("order_hint")
+        if h is not None:  # int32 [B] (dispatch_order 2), e.g. a previous solve's iters
+            out["order_hint"] = (h if isinstance(h, torch.Tensor) else torch.from_numpy(np.asarray(h))).to(
+                self.device, torch.int32).contiguous()
         for k in _IN_KEYS:
             v = batch.get(k)
             if v is None:
@@ -102,8 +106,12 @@ class BatchSolver:
             if tuple(v.shape) != shp or v.dtype != torch.float64 or not v.is_contiguous() or v.device != self.device:
                 raise ValueError(f"input {k}: expected contiguous float64 {shp} on {self.device}, got "
                                  f"{tuple(v.shape)} {v.dtype} {v.device}")
+        h = dev_in.get("order_hint")
+        if h is not None and (tuple(h.shape) != (B,) or h.dtype != torch.int32 or not h.is_contiguous()
+                              or h.device != self.device):
+            raise ValueError(f"input order_hint: expected contiguous int32 ({B},) on {self.device}")
         ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
-        inp = abi.MRInputs(*[ptr(dev_in.get(k)) for k in _IN_KEYS])
+        inp = abi.MRInputs(*[ptr(dev_in.get(k)) for k in _IN_KEYS + ("order_hint",)])
         tr = out.get("trace")
         o = abi.MROutputs(*[ptr(out.get(k)) for k in ("X", "U", "S", "eC", "eL", "status", "iters", "obj", "kkt",
                                                       "trace")], int(trace_instance),

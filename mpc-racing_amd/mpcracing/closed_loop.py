@@ -48,6 +48,9 @@ class ClosedLoop:
         self.plant = PLANT[plant]
         self.dt, self.start_control_at = float(dt), int(start_control_at)
         self.lookback, self.lookahead = float(lookback), float(lookahead)
+        # dispatch: longest-expected-first by the previous tick's iteration counts of the same vehicles
+        # (mr_config.dispatch_order 2, LPT with a distribution-agnostic estimate); results do not depend on it
+        solver_kw.setdefault("dispatch_order", 2)
         self.solver = BatchSolver(N, mpc_model, precision, False, Ts, max_batch=self.B, device=device, **solver_kw)
         f = dict(dtype=torch.float64, device=self.dev)
         # RuntimeControllerParameters (control/ControllerParameters.py:26-32) as (alpha_c, d_max, q_v_y, n,
@@ -123,7 +126,9 @@ class ClosedLoop:
                 lc = self.last_controls
                 u_init = torch.cat([lc[:, 1:], lc[:, -1:]], dim=1).contiguous()
             dev_in = dict(state0=state0, s0=self.progress, cx=self.cx, cy=self.cy, max_error=self.max_error,
-                          runtime=self.runtime, u_init=u_init)
+                          runtime=self.runtime, u_init=u_init,
+                          # the previous tick's iters, read by the order kernel before this solve writes them
+                          order_hint=self.sol["iters"] if self.last_controls is not None else None)
             self.solver.launch(dev_in, self.sol, stream=st)
             U = self.sol["U"]
             self.last_controls = U.clone()

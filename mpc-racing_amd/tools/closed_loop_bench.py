@@ -27,8 +27,10 @@ def main():
     T = int(sys.argv[2]) if len(sys.argv) > 2 else 40
     res = {}
     tr = DeviceTrack("shanghai_intl_circuit")
-    for prec in ("fp64", "fp32"):
-        loop = ClosedLoop(tr, B=B, N=15, plant="blend", precision=prec, start_control_at=1)
+    # fp64 in index order and in hint order (dispatch_order 2: the previous tick's iterations, the
+    # ClosedLoop default), fp32 in hint order
+    for prec, order in (("fp64", 0), ("fp64", 2), ("fp32", 2)):
+        loop = ClosedLoop(tr, B=B, N=15, plant="blend", precision=prec, start_control_at=1, dispatch_order=order)
         s0 = (np.arange(B) + 0.5) * tr.length / B
         loop.reset(ClosedLoop.start_states(tr, s0, v0=15.0))
         loop.run(2)  # global projections of the first tick, warm-up
@@ -40,11 +42,11 @@ def main():
         st = np.stack([r["status"].cpu().numpy() for r in recs])
         it = np.stack([r["iters"].cpu().numpy() for r in recs])
         err = np.abs(recs[-1]["error"].cpu().numpy())
-        res[prec] = {"B": B, "ticks": T, "s": dt, "ticks_per_s": T / dt, "vehicle_ticks_per_s": B * T / dt,
+        res[f"{prec}_order{order}"] = {"B": B, "dispatch_order": order, "ticks": T, "s": dt, "ticks_per_s": T / dt, "vehicle_ticks_per_s": B * T / dt,
                      "status_hist": np.bincount(st.ravel(), minlength=5).tolist(), "iters_mean": float(it.mean()),
                      "iters_max": int(it.max()), "abs_error_p50": float(np.median(err)),
                      "abs_error_max": float(err.max())}
-        print(prec, json.dumps(res[prec]), flush=True)
+        print(prec, order, json.dumps(res[f"{prec}_order{order}"]), flush=True)
     host_track = __import__("mpcracing.track", fromlist=["Track"]).Track("shanghai_intl_circuit")
     seg = ga.TrackSegments(host_track, 5, 30, 1500, 1500, 250)   # GA/mpcGA.py:31
     rng = np.random.default_rng(0)

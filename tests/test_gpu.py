@@ -268,3 +268,21 @@ def test_dispatch_order_does_not_change_results():
     o1 = _np(solver_for_config("C4", 3000, dispatch_order=1).solve(b))
     for k in o0:
         assert np.array_equal(o0[k], o1[k]), k
+
+
+def test_dispatch_order_hint_does_not_change_results():
+    """mr_config.dispatch_order = 2 (longest-expected-first by mr_inputs.order_hint, mr_order_hint_kernel):
+    bit-identical outputs to index order, with a real hint (the iterations of a first solve, as the
+    closed loop passes the previous tick's), with out-of-range hints (clamped buckets) and without one."""
+    import torch
+    b = wl.make_batch("C4", limit=3000)
+    o0 = _np(solver_for_config("C4", 3000, dispatch_order=0).solve(b))
+    s2 = solver_for_config("C4", 3000, dispatch_order=2)
+    rng = np.random.default_rng(7)
+    for hint in (o0["iters"].astype(np.int32), rng.integers(-50, 5000, 3000).astype(np.int32), None):
+        bb = dict(b, order_hint=hint) if hint is not None else b
+        o2 = _np(s2.solve(bb))
+        for k in o0:
+            assert np.array_equal(o0[k], o2[k]), k
+    with pytest.raises(ValueError):
+        s2.solve(dict(b, order_hint=torch.zeros(5, dtype=torch.int32)))

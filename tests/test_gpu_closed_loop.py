@@ -149,3 +149,31 @@ def test_ga_evaluate_population_matches_cpu_loop(dtrack):
     rr, aref = ga.rewards(tref, [1.0] * K)
     np.testing.assert_allclose(r, rr, rtol=1e-6)
     np.testing.assert_allclose(avg, aref, rtol=1e-6)
+
+
+def test_closed_loop_hint_order_matches_index_order(dtrack):
+    """The closed loop dispatches each tick's solves longest-expected-first by the previous tick's
+    iteration counts (dispatch_order 2, the default of ClosedLoop): bit-identical trajectories to index
+    order on a non-C4 state distribution (512 vehicles spread over the lap, the agent's own states), and
+    the per-tick solve time is reported for both (tools/order_probe.py records the comparison)."""
+    import time
+    from mpcracing.closed_loop import ClosedLoop
+    B, N, ticks, start = 512, 15, 10, 2
+    s0 = np.linspace(50.0, 5000.0, B)
+    x0 = ClosedLoop.start_states(dtrack, s0, v0=12.0, offset=0.2)
+    res = {}
+    for order in (0, 2):
+        loop = ClosedLoop(dtrack, B=B, N=N, plant="blend", start_control_at=start, dispatch_order=order)
+        loop.reset(x0)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        recs = loop.run(ticks)
+        torch.cuda.synchronize()
+        res[order] = (recs, time.perf_counter() - t)
+    for r0, r2 in zip(res[0][0], res[2][0]):
+        for k in ("X", "Y", "yaw", "vx", "vy", "progress", "cmd_throttle", "cmd_steer", "cmd_brake"):
+            assert torch.equal(r0[k], r2[k]), (r0["step"], k)
+        if r0["controlled"]:
+            assert torch.equal(r0["iters"], r2["iters"]) and torch.equal(r0["status"], r2["status"])
+    print("closed loop", B, "vehicles", ticks, "ticks: index order %.1f ms, hint order %.1f ms"
+          % (1e3 * res[0][1], 1e3 * res[2][1]))
