@@ -38,6 +38,17 @@ constexpr int NZS = NZ + 1;  // stored stage vector: z plus one unused slot (ind
 constexpr int JL = 14;       // slots 14, 15, 16: lane rows e_C + m + t >= 0, m - e_C + t >= 0, t >= 0
 constexpr int NH = NZ * (NZ + 1) / 2;  // packed upper triangle of the 14x14 stage Hessian
 constexpr int NP = NX * (NX + 1) / 2;  // packed P
+// IPOPT's inertia correction delta_w I regularises the NLP's own variables (the reference's States, S_hat
+// and U, control/MPC.py:62-64).  In the stage-wise restatement those are x_k[0..5], S = x_k[6] and
+// u_k[0..1]; the restatement's extra variables -- Delta-S (u_k[2]), the previous-control copy p (x_k[7..8])
+// and the frozen U[:,0] copy w (x_k[9..10]), each fixed by equality rows -- get no shift, so the regularised
+// Newton step is the one IPOPT computes in the reference's variables (a shift on the copies would add
+// further terms to the reference variables' diagonal through those rows).  MR_DELTA_ALL=1: every stage
+// variable shifted (the round-2 rule, A/B).
+#ifndef MR_DELTA_ALL
+#define MR_DELTA_ALL 0
+#endif
+MR_HD constexpr bool delta_var(int i) { return MR_DELTA_ALL ? i < NZ : (i <= 6 || i == 11 || i == 12); }
 
 // Workspace fields per stage (SoA: element (k, f) of instance i at base[(k*NF + f)*stride + i]).
 struct WF {
@@ -987,7 +998,7 @@ struct Solver {
     {
       const int k = N;
       for (int i = 0; i < NX; ++i)
-        for (int j = i; j < NX; ++j) Pm[pidx(i, j)] = W(k, WF::H + hidx(i, j)) + (i == j ? delta : T(0));
+        for (int j = i; j < NX; ++j) Pm[pidx(i, j)] = W(k, WF::H + hidx(i, j)) + (i == j && delta_var(i) ? delta : T(0));
       for (int i = 0; i < NX; ++i) { p0[i] = W(k, WF::G0 + i); p1[i] = W(k, WF::G1 + i); }
       for (int i = 0; i < NP; ++i) W(k, WF::P + i) = Pm[i];
       for (int i = 0; i < NX; ++i) { W(k, WF::PV0 + i) = p0[i]; W(k, WF::PV1 + i) = p1[i]; }
@@ -1034,7 +1045,7 @@ struct Solver {
             for (int i = 0; i < NX; ++i) colb[i] = PB[i][b];
             T bt[NU];
             apply_Bt(J, k, colb, bt);
-            Rh[q] = W(k, WF::H + hidx(NX + a, NX + b)) + bt[a] + (a == b ? delta : T(0));
+            Rh[q] = W(k, WF::H + hidx(NX + a, NX + b)) + bt[a] + (a == b && delta_var(NX + a) ? delta : T(0));
           }
       }
       T Sh[NU][NX];
@@ -1076,7 +1087,7 @@ struct Solver {
         for (int i = 0; i < NX; ++i) colj[i] = PA[i][j];
         apply_At(J, k, colj, at);  // column j of A^T P A
         for (int i = 0; i <= j; ++i) {
-          T v = at[i] + W(k, WF::H + hidx(i, j)) + (i == j ? delta : T(0));
+          T v = at[i] + W(k, WF::H + hidx(i, j)) + (i == j && delta_var(i) ? delta : T(0));
           for (int a = 0; a < NU; ++a) v += Sh[a][i] * Kg[a][j];
           Pn[pidx(i, j)] = v;
         }

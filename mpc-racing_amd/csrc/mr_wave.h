@@ -734,7 +734,7 @@ struct WaveSolver {
       const int a = drow(g, v);
       const int a_ = a < NZ ? a : 0;
       fp.off[4 + v] = a < NZ ? (c < NZ ? RCF::H + hidx(a_, c) : (c == 14 ? RCF::G0 + a_ : RCF::G1 + a_)) : RCF::CZERO;
-      if (a < NZ && a == c) fp.dlt |= 1u << v;
+      if (a < NZ && a == c && delta_var(a)) fp.dlt |= 1u << v;
       // outputs of D register v: packed-upper P | p0 | p1, LDS image of P^
       const int junk_r = RCF::JUNK, junk_l = LJUNK_OFF - LP_OFF + lane;  // lp* index from LP
       const bool ax = a < NX, up = ax & (c < NX) & (a <= c);
@@ -848,7 +848,7 @@ struct WaveSolver {
       const T p0 = rb.ld(Rn, RCF::G0 + lr), p1 = rb.ld(Rn, RCF::G1 + lr);
 #pragma unroll
       for (int j = 0; j < NX; ++j) {
-        const T v = hv[j] + (l == j ? delta : T(0));
+        const T v = hv[j] + (l == j && delta_var(j) ? delta : T(0));
         LP[row ? l * LDS_LD + j : jd] = v;
         rb.st(v, Rn, (row && j >= l) ? RCF::P + pidx(lr, j) : jl);
       }
@@ -1018,7 +1018,8 @@ struct WaveSolver {
       const T p0 = rb.ld(Rn, RCF::G0 + lr), p1 = rb.ld(Rn, RCF::G1 + lr);
 #pragma unroll
       for (int j = 0; j < NX; ++j) {
-        const T va = hv[j] + (l == j ? da : T(0)), vb = hv[j] + (l == j ? db : T(0));
+        const bool dj = l == j && delta_var(j);
+        const T va = hv[j] + (dj ? da : T(0)), vb = hv[j] + (dj ? db : T(0));
         LT[0][row ? l * LDS_LD + j : jda] = va;
         LT[1][row ? l * LDS_LD + j : jdb] = vb;
         const bool st = row && j >= l;
