@@ -1,0 +1,35 @@
+#!/bin/bash
+# Round-end GPU session on the committed build: parity tests, smoke, bench line, rocprofv3 kernel stats,
+# the two PMC passes (FETCH_SIZE / WRITE_SIZE, separate runs) and their summary, the PMC calibration
+# (tools/pmc_calib.hip: 1 GiB read / written at 4 and 8 B per lane), the C4 timeline and the other
+# configurations' bench lines.  Every GPU step has its own time limit; the session stops at the first
+# crash / timeout (test failures, rc 1, do not stop it).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # name limit cmd...
+  local name=$1 lim=$2; shift 2
+  echo "== $name: $*" >> gpurun_out/session.log
+  timeout -k 10 "$lim" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" >> gpurun_out/session.log
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+  return 0
+}
+B=$(python -c "import sys; sys.path.insert(0,'mpc-racing_amd'); from mpcracing import workload as wl; print(wl.CONFIGS['C4']['per_gpu'])")
+step pytest_gpu 900 python -u -m pytest tests -m gpu -v -rA --timeout 300 --timeout-method thread
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python bench.py
+step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-latency
+step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-latency
+step pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-latency
+step pmc_sum 120 python mpc-racing_amd/tools/pmc_summary.py gpurun_out/prof/run_kernel_stats.csv gpurun_out/pmc_fetch/run_counter_collection.csv gpurun_out/pmc_write/run_counter_collection.csv gpurun_out/pmc_C4.json mr_wave_kernel $B C4
+if [ -x variants/pmc_calib ]; then
+  step calib_fetch 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/calib_fetch -o run --output-format csv -- variants/pmc_calib
+  step calib_write 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/calib_write -o run --output-format csv -- variants/pmc_calib
+fi
+step timeline 300 python -u mpc-racing_amd/tools/timeline_probe.py C4 1
+for c in C2 C3 C5; do
+  step bench_$c 600 python bench.py --config $c --no-cpu-baseline
+done
