@@ -187,6 +187,10 @@ int mr_track_error_sign(const mr_track* tr, int32_t n, const double* X, const do
 /* x_as_coeffs / y_as_coeffs(s, lookahead, deg = 4): cx, cy [5][n], highest order first, global s */
 int mr_track_polyfit(const mr_track* tr, int32_t n, const double* s, const double* lookahead, double* cx,
                      double* cy, void* hip_stream);
+/* x_as_coeffs / y_as_coeffs with the reference's deg argument (splines/ParameterizedLine.py:43-64):
+   0 <= deg <= 10, cx, cy [deg + 1][n], highest order first, global s (deg 4 = mr_track_polyfit) */
+int mr_track_polyfit_deg(const mr_track* tr, int32_t n, const double* s, const double* lookahead, int32_t deg,
+                         double* cx, double* cy, void* hip_stream);
 /* lookup_error(s, lookahead) -> err [n] (NaN where the reference raises KeyError); row_lo / row_hi /
    row_arg [n]: first / last / arg-min lane-table row (-1 on KeyError; each may be NULL) */
 int mr_track_lookup_error(const mr_track* tr, int32_t n, const double* s, const double* lookahead, double* err,

@@ -323,6 +323,16 @@ __global__ __launch_bounds__(kTrackBlock) void mr_track_polyfit_kernel(TrackView
   for (int j = 0; j < 5; ++j) { cx[(int64_t)j * n + i] = a[j]; cy[(int64_t)j * n + i] = b[j]; }
 }
 
+__global__ __launch_bounds__(kTrackBlock) void mr_track_polyfit_deg_kernel(TrackView T, int n, const double* s,
+                                                                           const double* la, int deg, double* cx,
+                                                                           double* cy) {
+  const int i = blockIdx.x * kTrackBlock + threadIdx.x;
+  if (i >= n) return;
+  double a[MR_POLY_DEG_MAX + 1], b[MR_POLY_DEG_MAX + 1];
+  if (!track_polyfit_deg(T, s[i], la[i], deg, a, b)) return;
+  for (int j = 0; j <= deg; ++j) { cx[(int64_t)j * n + i] = a[j]; cy[(int64_t)j * n + i] = b[j]; }
+}
+
 __global__ __launch_bounds__(kTrackBlock) void mr_track_lookup_kernel(TrackView T, int n, const double* s,
                                                                       const double* la, double* err, int32_t* rlo,
                                                                       int32_t* rhi, int32_t* rarg) {
@@ -614,6 +624,13 @@ int mr_track_polyfit(const mr_track* tr, int32_t n, const double* s, const doubl
                      void* hip_stream) {
   if (!s || !lookahead || !cx || !cy) return fail(MR_ERR_ARG, "null argument");
   MR_TRACK_LAUNCH(mr_track_polyfit_kernel, s, lookahead, cx, cy);
+}
+
+int mr_track_polyfit_deg(const mr_track* tr, int32_t n, const double* s, const double* lookahead, int32_t deg,
+                         double* cx, double* cy, void* hip_stream) {
+  if (!s || !lookahead || !cx || !cy) return fail(MR_ERR_ARG, "null argument");
+  if (deg < 0 || deg > MR_POLY_DEG_MAX) return fail(MR_ERR_ARG, "deg out of range (0..10)");
+  MR_TRACK_LAUNCH(mr_track_polyfit_deg_kernel, s, lookahead, (int)deg, cx, cy);
 }
 
 int mr_track_lookup_error(const mr_track* tr, int32_t n, const double* s, const double* lookahead, double* err,

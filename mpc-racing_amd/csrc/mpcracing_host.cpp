@@ -168,6 +168,16 @@ int mrh_track_polyfit(const double* blob, int nt, double L, int n_rows, int n, c
   }
   return 0;
 }
+int mrh_track_polyfit_deg(const double* blob, int nt, double L, int n_rows, int n, const double* s, const double* la,
+                          int deg, double* cx, double* cy) {
+  TrackView T = track_view(blob, nt, L, n_rows);
+  for (int i = 0; i < n; ++i) {
+    double a[MR_POLY_DEG_MAX + 1], b[MR_POLY_DEG_MAX + 1];
+    if (!track_polyfit_deg(T, s[i], la[i], deg, a, b)) return -1;
+    for (int j = 0; j <= deg; ++j) { cx[(int64_t)j * n + i] = a[j]; cy[(int64_t)j * n + i] = b[j]; }
+  }
+  return 0;
+}
 int mrh_track_lookup(const double* blob, int nt, double L, int n_rows, int n, const double* s, const double* la,
                      double* err, int* lo, int* hi, int* arg) {
   TrackView T = track_view(blob, nt, L, n_rows);

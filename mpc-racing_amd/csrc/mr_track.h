@@ -319,72 +319,100 @@ MR_HD int track_error_sign(const TrackView& T, double X, double Y, double s) {
   return a < b ? 1 : -1;
 }
 
-// x_as_coeffs / y_as_coeffs(s, lookahead, deg=4): least-squares quartic through the 50 samples of
-// G on numpy.linspace(0, lookahead, 50) + s, in GLOBAL s, highest order first (np.polyfit).
-// Normal equations in u = (s' - mid) / h (moments of a well-conditioned basis), Cholesky 5x5,
-// then the exact binomial expansion back to powers of s'.
-MR_HD void track_polyfit(const TrackView& T, double s, double lookahead, double* cx, double* cy) {
+// x_as_coeffs / y_as_coeffs(s, lookahead, deg) (ParameterizedLine.py:43-64): least-squares polynomial of
+// degree D through the 50 samples of G on numpy.linspace(0, lookahead, 50) + s, in GLOBAL s, highest
+// order first (np.polyfit).  Normal equations in u = (s' - mid) / h (moments of a well-conditioned
+// basis), Cholesky, then the exact binomial expansion back to powers of s'.  D = 4 is the agent's fit
+// (agent.py:140); the others serve the drop-in's deg argument (D <= MR_POLY_DEG_MAX).
+constexpr int MR_POLY_DEG_MAX = 10;
+template <int D>
+MR_HD void track_polyfit_t(const TrackView& T, double s, double lookahead, double* cx, double* cy) {
+  constexpr int K = D + 1;
   const int M = 50;
   const double h = lookahead > 0 ? 0.5 * lookahead : 1.0;
   const double mid = s + 0.5 * lookahead;
   const double step = lookahead / (M - 1);
-  double mom[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, rx[5] = {0, 0, 0, 0, 0}, ry[5] = {0, 0, 0, 0, 0};
+  double mom[2 * D + 1], rx[K], ry[K];
+  for (int j = 0; j <= 2 * D; ++j) mom[j] = 0.0;
+  for (int j = 0; j < K; ++j) { rx[j] = 0.0; ry[j] = 0.0; }
   for (int i = 0; i < M; ++i) {
     const double q = (i == M - 1 ? lookahead : i * step) + s;
     const double m = py_mod(q, T.L);
     const double yx = spline_eval(T.x[0], m), yy = spline_eval(T.y[0], m);
     const double u = (q - mid) / h;
     double p = 1.0;
-    for (int j = 0; j < 9; ++j) {
+    for (int j = 0; j <= 2 * D; ++j) {
       mom[j] += p;
-      if (j < 5) { rx[j] += p * yx; ry[j] += p * yy; }
+      if (j < K) { rx[j] += p * yx; ry[j] += p * yy; }
       p *= u;
     }
   }
-  double G[5][5], L[5][5];
-  for (int i = 0; i < 5; ++i)
-    for (int j = 0; j < 5; ++j) { G[i][j] = mom[i + j]; L[i][j] = 0.0; }
-  for (int j = 0; j < 5; ++j) {
-    double d = G[j][j];
+  double L[K][K];
+  for (int i = 0; i < K; ++i)
+    for (int j = 0; j < K; ++j) L[i][j] = 0.0;
+  for (int j = 0; j < K; ++j) {
+    double d = mom[2 * j];
     for (int q = 0; q < j; ++q) d -= L[j][q] * L[j][q];
     L[j][j] = sqrt(d);
-    for (int i = j + 1; i < 5; ++i) {
-      double v = G[i][j];
+    for (int i = j + 1; i < K; ++i) {
+      double v = mom[i + j];
       for (int q = 0; q < j; ++q) v -= L[i][q] * L[j][q];
       L[i][j] = v / L[j][j];
     }
   }
-  double ax[5], ay[5];
-  for (int i = 0; i < 5; ++i) {  // L y = r
+  double ax[K], ay[K];
+  for (int i = 0; i < K; ++i) {  // L y = r
     double vx = rx[i], vy = ry[i];
     for (int q = 0; q < i; ++q) { vx -= L[i][q] * ax[q]; vy -= L[i][q] * ay[q]; }
     ax[i] = vx / L[i][i];
     ay[i] = vy / L[i][i];
   }
-  for (int i = 4; i >= 0; --i) {  // L^T a = y
+  for (int i = K - 1; i >= 0; --i) {  // L^T a = y
     double vx = ax[i], vy = ay[i];
-    for (int q = i + 1; q < 5; ++q) { vx -= L[q][i] * ax[q]; vy -= L[q][i] * ay[q]; }
+    for (int q = i + 1; q < K; ++q) { vx -= L[q][i] * ax[q]; vy -= L[q][i] * ay[q]; }
     ax[i] = vx / L[i][i];
     ay[i] = vy / L[i][i];
   }
   // sum_j a_j ((s' - mid) / h)^j  ->  ascending powers of s'
-  const double binom[5][5] = {{1, 0, 0, 0, 0}, {1, 1, 0, 0, 0}, {1, 2, 1, 0, 0}, {1, 3, 3, 1, 0}, {1, 4, 6, 4, 1}};
-  double gx[5] = {0, 0, 0, 0, 0}, gy[5] = {0, 0, 0, 0, 0};
+  double gx[K], gy[K];
+  for (int j = 0; j < K; ++j) { gx[j] = 0.0; gy[j] = 0.0; }
   double hj = 1.0;
-  for (int j = 0; j < 5; ++j) {
+  for (int j = 0; j < K; ++j) {
     const double sx = ax[j] / hj, sy = ay[j] / hj;
-    for (int i = 0; i <= j; ++i) {
-      double pm = 1.0;
-      for (int q = 0; q < j - i; ++q) pm *= -mid;
-      gx[i] += sx * binom[j][i] * pm;
-      gy[i] += sy * binom[j][i] * pm;
+    double bin = 1.0;  // C(j, i), from i = j down
+    double pm = 1.0;   // (-mid)^(j - i)
+    for (int i = j; i >= 0; --i) {
+      gx[i] += sx * bin * pm;
+      gy[i] += sy * bin * pm;
+      bin = bin * (double)i / (double)(j - i + 1);
+      pm *= -mid;
     }
     hj *= h;
   }
-  for (int j = 0; j < 5; ++j) {
-    cx[j] = gx[4 - j];
-    cy[j] = gy[4 - j];
+  for (int j = 0; j < K; ++j) {
+    cx[j] = gx[D - j];
+    cy[j] = gy[D - j];
   }
+}
+MR_HD void track_polyfit(const TrackView& T, double s, double lookahead, double* cx, double* cy) {
+  track_polyfit_t<4>(T, s, lookahead, cx, cy);
+}
+// any degree 0..MR_POLY_DEG_MAX (false otherwise); cx, cy hold deg + 1 coefficients
+MR_HD bool track_polyfit_deg(const TrackView& T, double s, double lookahead, int deg, double* cx, double* cy) {
+  switch (deg) {
+    case 0: track_polyfit_t<0>(T, s, lookahead, cx, cy); return true;
+    case 1: track_polyfit_t<1>(T, s, lookahead, cx, cy); return true;
+    case 2: track_polyfit_t<2>(T, s, lookahead, cx, cy); return true;
+    case 3: track_polyfit_t<3>(T, s, lookahead, cx, cy); return true;
+    case 4: track_polyfit_t<4>(T, s, lookahead, cx, cy); return true;
+    case 5: track_polyfit_t<5>(T, s, lookahead, cx, cy); return true;
+    case 6: track_polyfit_t<6>(T, s, lookahead, cx, cy); return true;
+    case 7: track_polyfit_t<7>(T, s, lookahead, cx, cy); return true;
+    case 8: track_polyfit_t<8>(T, s, lookahead, cx, cy); return true;
+    case 9: track_polyfit_t<9>(T, s, lookahead, cx, cy); return true;
+    case 10: track_polyfit_t<10>(T, s, lookahead, cx, cy); return true;
+  }
+  return false;
 }
 
 // Host: the device tables of one track from the scipy spline (t, c, k = 3): G's coefficients

@@ -45,7 +45,7 @@ class MROutputs(ctypes.Structure):
 EXPORTS = ["mr_version", "mr_last_error", "mr_config_default", "mr_create", "mr_destroy", "mr_set_tyres",
            "mr_solve_batch", "mr_workspace_bytes_per_instance", "mr_eval_dynamics",
            "mr_track_create", "mr_track_destroy", "mr_track_eval", "mr_track_frame", "mr_track_error_sign",
-           "mr_track_polyfit", "mr_track_lookup_error", "mr_track_projection", "mr_track_prep",
+           "mr_track_polyfit", "mr_track_polyfit_deg", "mr_track_lookup_error", "mr_track_projection", "mr_track_prep",
            "mr_spline_from_waypoints", "mr_track_lane_table", "mr_agent_sense", "mr_plant_step"]
 
 
@@ -68,6 +68,7 @@ def _bind_product(lib):
     lib.mr_track_frame.argtypes = [V, _I32, V, V, V, V, V, _D, V, V]
     lib.mr_track_error_sign.argtypes = [V, _I32, V, V, V, V, V]
     lib.mr_track_polyfit.argtypes = [V, _I32, V, V, V, V, V]
+    lib.mr_track_polyfit_deg.argtypes = [V, _I32, V, V, _I32, V, V, V]
     lib.mr_track_lookup_error.argtypes = [V, _I32, V, V, V, V, V, V, V]
     lib.mr_track_projection.argtypes = [V, _I32, V, V, V, V, V, V, V, V]
     lib.mr_track_prep.argtypes = [V, _I32, V, V, V, V, _D, _D, _D, V, V, V, V, V, V]
@@ -113,6 +114,7 @@ def load_host_twin(path=HOST_TWIN_LIB):
     lib.mrh_track_frame.argtypes = [V, I, _D, I, I, V, V, V, V, V, _D, V]
     lib.mrh_track_sign.argtypes = [V, I, _D, I, I, V, V, V, V]
     lib.mrh_track_polyfit.argtypes = [V, I, _D, I, I, V, V, V, V]
+    lib.mrh_track_polyfit_deg.argtypes = [V, I, _D, I, I, V, V, I, V, V]
     lib.mrh_track_lookup.argtypes = [V, I, _D, I, I, V, V, V, V, V, V]
     lib.mrh_track_projection.argtypes = [V, I, _D, I, I, V, V, V, V, V, V, V]
     lib.mrh_spline_from_waypoints.argtypes = [_PD, _PD, I, I, _PD, _PD, _PD, _PI32, _PD]

@@ -130,14 +130,19 @@ class DeviceTrack:
                                                  self._stream(stream)))
         return sg
 
-    def polyfit(self, s, lookahead, stream=None):
-        """x_as_coeffs / y_as_coeffs: cx, cy [5][n], highest order first, global s."""
+    def polyfit(self, s, lookahead, stream=None, deg=4):
+        """x_as_coeffs / y_as_coeffs: cx, cy [deg+1][n], highest order first, global s (0 <= deg <= 10)."""
         s = self._d(s)
         la = self._d(np.broadcast_to(np.asarray(lookahead, dtype=np.float64), (s.numel(),)).copy()
                      if not isinstance(lookahead, torch.Tensor) else lookahead)
         n = s.numel()
-        cx, cy = self._f(5, n), self._f(5, n)
-        self._check(self.lib.mr_track_polyfit(self.h, n, _ptr(s), _ptr(la), _ptr(cx), _ptr(cy), self._stream(stream)))
+        cx, cy = self._f(deg + 1, n), self._f(deg + 1, n)
+        if deg == 4:
+            self._check(self.lib.mr_track_polyfit(self.h, n, _ptr(s), _ptr(la), _ptr(cx), _ptr(cy),
+                                                  self._stream(stream)))
+        else:
+            self._check(self.lib.mr_track_polyfit_deg(self.h, n, _ptr(s), _ptr(la), int(deg), _ptr(cx), _ptr(cy),
+                                                      self._stream(stream)))
         return cx, cy
 
     def lookup_error(self, s, lookahead, stream=None):

@@ -92,15 +92,14 @@ class ParameterizedLine:
 
     # ---- local polynomial (:43-64) ----
     def x_as_coeffs(self, s, lookahead, deg=4):
-        if deg != 4:
-            raise NotImplementedError("the device fit is the agent's quartic (POLY_DEG = 4, agent.py:140)")
-        cx, _ = self.dev.polyfit([s], lookahead)
+        """deg 0..10 on the device (mr_track_polyfit_deg); the reference's np.polyfit takes any degree but
+        warns that high ones are ill-conditioned -- above 10 the global-s monomial coefficients carry no
+        digits in fp64."""
+        cx, _ = self.dev.polyfit([s], lookahead, deg=int(deg))
         return list(cx[:, 0].cpu().numpy())
 
     def y_as_coeffs(self, s, lookahead, deg=4):
-        if deg != 4:
-            raise NotImplementedError("the device fit is the agent's quartic (POLY_DEG = 4, agent.py:140)")
-        _, cy = self.dev.polyfit([s], lookahead)
+        _, cy = self.dev.polyfit([s], lookahead, deg=int(deg))
         return list(cy[:, 0].cpu().numpy())
 
     # ---- projection (:66-105) ----

@@ -133,3 +133,22 @@ def test_dropin_line_from_waypoints():
     ps, dist = lane.projection(cl.Gx(s0), cl.Gy(s0), bounds=None)
     assert lane.last_progress == ps and dist > 0
     assert cl.lookup_error(s0, 45.0) == wl.track("t4").lookup_error(s0, 45.0)
+
+
+def test_polyfit_any_degree_matches_host_build(dev):
+    """mr_track_polyfit_deg (the reference's deg argument, ParameterizedLine.py:43-64) on the device is
+    bit-exact against the host build of the same source for every supported degree (0..10; the CPU suite
+    checks those against numpy.polyfit), deg 4 equals mr_track_polyfit, and deg 11 is an argument error."""
+    from track_twin import HostTrack
+    track, d = dev
+    p = track + "/"
+    ht = HostTrack(G, track)
+    s, la = G[p + "g3_s"], G[p + "g3_la"]
+    for deg in range(0, 11):
+        cx, cy = d.polyfit(s, torch.tensor(la), deg=deg)
+        hx, hy = ht.polyfit_deg(s, la, deg)
+        assert np.array_equal(_np(cx), hx) and np.array_equal(_np(cy), hy), deg
+    q4 = d.polyfit(s, torch.tensor(la))
+    assert np.array_equal(_np(q4[0]), ht.polyfit_deg(s, la, 4)[0])
+    with pytest.raises(RuntimeError):
+        d.polyfit(s, torch.tensor(la), deg=11)

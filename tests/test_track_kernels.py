@@ -86,3 +86,26 @@ def test_lookup_error_keyerror_is_nan():
     err, lo, hi, arg = ht.lookup([60.0, 10.0], [5.0, 5.0])
     assert np.isnan(err[0]) and lo[0] == -1 and arg[0] == -1
     assert err[1] == min(ht.el[20:30].min(), ht.er[20:30].min())
+
+
+@pytest.mark.parametrize("deg,tol", [(0, 1e-9), (1, 1e-9), (2, 1e-9), (3, 1e-8), (4, 5e-7), (5, 1e-4)])
+def test_polyfit_any_degree(trk, deg, tol):
+    """x_as_coeffs / y_as_coeffs with the reference's deg argument (ParameterizedLine.py:43-64,
+    mr_track_polyfit_deg) against numpy.polyfit on the same spline samples, on the fitted VALUES over the
+    window.  The tolerance grows with the degree because both sides evaluate monomials in global s
+    (s up to 1 900 m here): from deg 6 on numpy itself warns that the fit is poorly conditioned and the
+    two differ by centimetres and more -- the reference's "please don't make this too high"."""
+    track, ht = trk
+    p = track + "/"
+    s, la = G[p + "g3_s"], G[p + "g3_la"]
+    cx, cy = ht.polyfit_deg(s, la, deg)
+    assert cx.shape == (deg + 1, len(s))
+    for i in range(len(s)):
+        ss = np.linspace(0, la[i], 50) + s[i]
+        g = ht.eval(ss)[0]
+        for c, y in ((cx, g[0]), (cy, g[1])):
+            ref = np.polyfit(ss, y, deg)
+            assert np.abs(np.polyval(c[:, i], ss) - np.polyval(ref, ss)).max() < tol
+    if deg == 4:  # the general path reproduces the agent's quartic bit for bit
+        qx, qy = ht.polyfit(s, la)
+        assert np.array_equal(qx, cx) and np.array_equal(qy, cy)

@@ -63,6 +63,14 @@ class HostTrack:
         self.lib.mrh_track_polyfit(_p(self.blob), self.nt, self.L, self.nr, len(s), _p(s), _p(la), _p(cx), _p(cy))
         return cx, cy
 
+    def polyfit_deg(self, s, la, deg):
+        s, la = self._a(s), self._a(la)
+        cx, cy = np.zeros((deg + 1, len(s))), np.zeros((deg + 1, len(s)))
+        rc = self.lib.mrh_track_polyfit_deg(_p(self.blob), self.nt, self.L, self.nr, len(s), _p(s), _p(la), deg,
+                                           _p(cx), _p(cy))
+        assert rc == 0
+        return cx, cy
+
     def lookup(self, s, la):
         s, la = self._a(s), self._a(la)
         n = len(s)
