@@ -17,7 +17,9 @@ models/BlendedBicycleModel.py:24-26, models/VehicleParameters.py:37-38): the dyn
 differentiable there, and the interior-point iteration cycles when the optimum puts predicted speeds on
 a corner.  Reported for every unsolved instance and, for comparison, over all solved ones.
 
-Usage: python mpc-racing_amd/tools/convergence_audit.py C3 1024 [max_checked] > profiles/r03_audit_C3.json
+Usage: python mpc-racing_amd/tools/convergence_audit.py C3 1024 [max_checked] [part/parts] > part.json
+(part/parts: audit only every parts-th unsolved instance, starting at part -- parallel shards; the
+shards' JSON outputs are merged with tools/merge_audit.py)
 """
 import json
 import os
@@ -69,6 +71,10 @@ def main():
         rec["solved_corner"] = {"n": int(ok.size), "frac_with_stage_within_0.05": float((cs[:, 1] > 0).mean()),
                                 "median_min_dist": float(np.median(cs[:, 0]))}
     bad = np.nonzero(o["status"] >= 2)[0][:max_checked]
+    if len(sys.argv) > 4:
+        part, parts = (int(x) for x in sys.argv[4].split("/"))
+        bad = bad[part::parts]
+        rec["shard"] = sys.argv[4]
     insts = wl.instance_dicts(b)
     T = lambda a: torch.tensor(a, dtype=torch.float64)  # noqa: E731
     for i in bad:
