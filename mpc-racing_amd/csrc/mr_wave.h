@@ -450,8 +450,8 @@ struct WaveSolver {
     load_z(cur, z);
     T nun[NX], znext[NX];
     for (int i = 0; i < NX; ++i) {
-      nun[i] = wshfl(w, nuk[i], nxt());
-      znext[i] = wshfl(w, z[i], nxt());
+      nun[i] = wnext(w, nuk[i]);
+      znext[i] = wnext(w, z[i]);
     }
 #if MR_PHASE_CYCLES
     const unsigned long long te0 = trace ? MR_CLOCK() : 0ull;
@@ -516,7 +516,7 @@ struct WaveSolver {
     // absolute form (nu_new = P dx + p with p ~ nu ~ 1e3) cannot resolve the stationarity below the
     // fp32 ulp of the costates (1.2e-4 at 1e3), above a 1e-4 tolerance.
     double nnd[NX];
-    for (int i = 0; i < NX; ++i) nnd[i] = wshfl(w, (own() && k >= 1) ? NUd(i) : 0.0, nxt());
+    for (int i = 0; i < NX; ++i) nnd[i] = wnext(w, (own() && k >= 1) ? NUd(i) : 0.0);
     if (own()) {
       double dd[NZ];
       for (int i = 0; i < NZ; ++i) dd[i] = 0.0;
@@ -1576,7 +1576,7 @@ struct WaveSolver {
           for (int i = 0; i < NX; ++i) zt[i] = myx[i];
       }
       T ztn[NX];
-      for (int i = 0; i < NX; ++i) ztn[i] = wshfl(w, zt[i], nxt());
+      for (int i = 0; i < NX; ++i) ztn[i] = wnext(w, zt[i]);
       T th_l = T(0), f_l = T(0), lg_l = T(0), lgr_l = T(0), tho_l = T(0), fo_l = T(0);
       int ok_l = 1;
       if (own()) {

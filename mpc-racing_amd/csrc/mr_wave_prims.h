@@ -62,6 +62,18 @@ __device__ __forceinline__ float wxor(const Wv&, float v, int m) { return __shfl
 __device__ __forceinline__ double wxor(const Wv&, double v, int m) { return __shfl_xor(v, m, 64); }
 __device__ __forceinline__ int wxor(const Wv&, int v, int m) { return __shfl_xor(v, m, 64); }
 
+// value of lane (lane + 1) mod 64 (the next stage's): one DPP row-crossing rotate (v_mov_b32_dpp wave_rol:1),
+// a VALU move instead of a ds_bpermute through the CU's LDS crossbar
+__device__ __forceinline__ float wnext(const Wv&, float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x134, 0xf, 0xf, false));
+}
+__device__ __forceinline__ double wnext(const Wv&, double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffLL), 0x134, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x134, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
 // value of lane src (src wave-uniform): v_readlane, result lands in an SGPR
 __device__ __forceinline__ int wbcast(const Wv&, int v, int src) { return __builtin_amdgcn_readlane(v, src); }
 __device__ __forceinline__ float wbcast(const Wv&, float v, int src) {
@@ -301,6 +313,8 @@ inline T wshfl(const Wv& w, T v, int src) {
   w.hw->barrier();
   return r;
 }
+template <typename T>
+inline T wnext(const Wv& w, T v) { return wshfl(w, v, (w.lane + 1) % WL); }
 template <typename T>
 inline T wbcast(const Wv& w, T v, int src) { return wshfl(w, v, src); }
 template <typename T>
