@@ -49,6 +49,16 @@ constexpr int NP = NX * (NX + 1) / 2;  // packed P
 #define MR_DELTA_ALL 0
 #endif
 MR_HD constexpr bool delta_var(int i) { return MR_DELTA_ALL ? i < NZ : (i <= 6 || i == 11 || i == 12); }
+// IPOPT's optimality error (scaled stationarity, primal and complementarity) measured on the reference's NLP
+// rather than the restatement: the stationarity of each reference variable is the sum of its restated
+// copies' (U_k = u_k[0..1] + p_{k+1} (+ every w_j for U_0); S_k = S_k + Delta-S_{k-1} - Delta-S_k), the
+// equality multipliers are the vehicle rows' nu_k[0..5] plus those of the initial-state rows X_0 = state0,
+// S_0 = s0, which the restatement eliminates and which are therefore carried as nu_0[0..6] (stepped by the
+// stage-0 costate, P_0 dx_0 + p_0 with dx_0 = 0), m_e = 6N + 7.  The restoration phase keeps the
+// restatement's measure.  MR_KKT_RESTATED=1: the restatement's measure throughout (round 2, A/B).
+#ifndef MR_KKT_RESTATED
+#define MR_KKT_RESTATED 0
+#endif
 
 // Workspace fields per stage (SoA: element (k, f) of instance i at base[(k*NF + f)*stride + i]).
 struct WF {
@@ -786,8 +796,15 @@ struct Solver {
     slam_max = T(0);
     slam_min = T(1e30);
     nu1 = lam1 = fval = logs = T(0);
-    me = NX * (N + 1);
+    const bool refk = !MR_KKT_RESTATED && !resto;  // the optimality error on the reference's NLP
+    me = refk ? 6 * N + 7 : NX * (N + 1);
     mi = 0;
+    if (refk)  // multipliers of the initial-state rows X_0 = state0, S_0 = s0 (lazy update, as nu_{k >= 1})
+      for (int i = 0; i <= 6; ++i) {
+        nub[0][i] += (double)alpha_p * (double)W(0, WF::DNU + i);
+        nu1 += mr_abs(T(nub[0][i]));
+      }
+    T sref_b = T(0), sref_u[2] = {T(0), T(0)}, sref_u0[2] = {T(0), T(0)}, sref_w[2] = {T(0), T(0)};
     T z[NZS], znext[NZS], nun[NX];
     load_z(0, cur, z);
     for (int k = 0; k <= N; ++k) {
@@ -798,7 +815,7 @@ struct Solver {
           const double v = nub[k + 1][i] + (double)alpha_p * (double)W(k + 1, WF::DNU + i);
           nub[k + 1][i] = v;
           nun[i] = T(v);
-          nu1 += mr_abs(nun[i]);
+          if (!refk || i < 6) nu1 += mr_abs(nun[i]);
         }
         load_z(k + 1, cur, znext);
 #ifdef MR_DEBUG_PRINT
@@ -867,7 +884,7 @@ struct Solver {
         apply_At(J, k, nub[k + 1], dd);
         apply_Bt(J, k, nub[k + 1], dd + NX);
       }
-      if (k >= 1)
+      if (k >= 1 || refk)  // (k = 0: nu_0 of the initial-state rows, zero unless refk)
         for (int i = 0; i < NX; ++i) dd[i] -= nub[k][i];
       // cost: the scaled objective, or the restoration phase's proximity term
       Err<T> e;
@@ -967,9 +984,28 @@ struct Solver {
         }
       }
       // stationarity: x-part for k >= 1, u-part for k < N
-      for (int i = 0; i < NZ; ++i) {
-        const T sti = T((double)st[i] + dd[i]);
-        if (i < NX ? k >= 1 : k < N) stat_max = mr_max(stat_max, mr_abs(sti));
+      if (refk) {  // of the reference's variables (States, S_hat, U), see MR_KKT_RESTATED
+        T sti[NZ];
+        for (int i = 0; i < NZ; ++i) sti[i] = T((double)st[i] + dd[i]);
+        for (int i = 0; i < 6; ++i) stat_max = mr_max(stat_max, mr_abs(sti[i]));  // X_k (k = 0: + nu_0)
+        const T b = k < N ? sti[13] : T(0);
+        stat_max = mr_max(stat_max, mr_abs(sti[6] + sref_b - b));  // S_k
+        sref_b = b;
+        if (k >= 1) {  // U_{k-1} with its copy p_k; U_0 waits for the w copies
+          for (int a = 0; a < 2; ++a) {
+            const T u = sref_u[a] + sti[7 + a];
+            if (k == 1) sref_u0[a] = u; else stat_max = mr_max(stat_max, mr_abs(u));
+            sref_w[a] += sti[9 + a];
+          }
+        }
+        if (k < N) { sref_u[0] = sti[11]; sref_u[1] = sti[12]; }
+        if (k == N)
+          for (int a = 0; a < 2; ++a) stat_max = mr_max(stat_max, mr_abs(sref_u0[a] + sref_w[a]));
+      } else {
+        for (int i = 0; i < NZ; ++i) {
+          const T sti = T((double)st[i] + dd[i]);
+          if (i < NX ? k >= 1 : k < N) stat_max = mr_max(stat_max, mr_abs(sti));
+        }
       }
       for (int i = 0; i < NH; ++i) W(k, WF::H + i) = H[i];
       for (int i = 0; i < NZ; ++i) {
@@ -1124,6 +1160,8 @@ struct Solver {
     gphi = T(0);
     T dx[NX];
     for (int i = 0; i < NX; ++i) dx[i] = T(0);
+    if (!MR_KKT_RESTATED && !resto)  // the initial-state rows' multiplier step: stage 0's costate (dx_0 = 0)
+      for (int i = 0; i < NX; ++i) W(0, WF::DNU + i) = W(0, WF::PV0 + i) + mu * W(0, WF::PV1 + i);
     T z[NZS];
     for (int k = 0; k <= N; ++k) {
       T dz[NZS];

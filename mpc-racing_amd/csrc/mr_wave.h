@@ -436,6 +436,9 @@ struct WaveSolver {
     int mi_l = 0;
     // lazy multiplier update nu_k += alpha_p * dnu_k (stages 1..N), in fp64; T copies weight the
     // dynamics Hessian
+    // refk: the optimality error on the reference's NLP (mr_solver.h MR_KKT_RESTATED); nu_0[0..6] = the
+    // multipliers of the initial-state rows X_0 = state0, S_0 = s0 (stepped by the stage-0 costate)
+    constexpr bool refk = !MR_KKT_RESTATED && !RESTO;
     T nuk[NX];
     for (int i = 0; i < NX; ++i) nuk[i] = T(0);
     if (own() && k >= 1) {
@@ -443,7 +446,13 @@ struct WaveSolver {
         const double v = NUd(i) + (double)alpha_p * (double)S(SSF::DNU + i);
         NUd(i) = v;
         nuk[i] = T(v);
-        nu1_l += mr_abs(nuk[i]);
+        if (!refk || i < 6) nu1_l += mr_abs(nuk[i]);
+      }
+    } else if (refk && k == 0) {
+      for (int i = 0; i <= 6; ++i) {
+        const double v = NUd(i) + (double)alpha_p * (double)S(SSF::DNU + i);
+        NUd(i) = v;
+        nu1_l += mr_abs(T(v));
       }
     }
     T z[NZS];
@@ -461,6 +470,7 @@ struct WaveSolver {
     const WBuf<T> rbe(rc, (unsigned)WL * (unsigned)RC_STRIDE);
     const unsigned Rk = (unsigned)k * (unsigned)RC_STRIDE;
     T H[NH], g0[NZ], g1[NZ], gl[NZ], st[NZ], J[48];
+    T rs_a = T(0), rs_b = T(0), rs_u[2] = {T(0), T(0)}, rs_p[2] = {T(0), T(0)}, rs_w[2] = {T(0), T(0)};
     if (own()) {
       for (int i = 0; i < NH; ++i) H[i] = T(0);
       for (int i = 0; i < NZ; ++i) { g0[i] = g1[i] = gl[i] = st[i] = T(0); }
@@ -524,7 +534,7 @@ struct WaveSolver {
         apply_At(J, k, nnd, dd);
         apply_Bt(J, k, nnd, dd + NX);
       }
-      if (k >= 1)
+      if (k >= 1 || refk)  // (k = 0: nu_0 of the initial-state rows, zero unless refk)
         for (int i = 0; i < NX; ++i) dd[i] -= NUd(i);
       Err<T> e;
       errors(I, z[0], z[1], z[6], e, true);
@@ -637,14 +647,36 @@ struct WaveSolver {
             H[hidx(id3[a], id3[bb])] += (sig0 + sig1) * e.gC[a] * e.gC[bb] - lamdiff * e.hC[q];
         }
       }
-      for (int i = 0; i < NZ; ++i) {
-        const T sti = T((double)st[i] + dd[i]);
-        if (i < NX ? k >= 1 : k < N) st_l = mr_max(st_l, mr_abs(sti));
+      if constexpr (refk) {  // the reference's variables: X_k here, S_k and U_k with their copies below
+        T sti[NZ];
+        for (int i = 0; i < NZ; ++i) sti[i] = T((double)st[i] + dd[i]);
+        for (int i = 0; i < 6; ++i) st_l = mr_max(st_l, mr_abs(sti[i]));
+        rs_a = sti[6];
+        rs_b = k < N ? sti[13] : T(0);
+        if (k < N) { rs_u[0] = sti[11]; rs_u[1] = sti[12]; }
+        if (k >= 1) { rs_p[0] = sti[7]; rs_p[1] = sti[8]; rs_w[0] = sti[9]; rs_w[1] = sti[10]; }
+      } else {
+        for (int i = 0; i < NZ; ++i) {
+          const T sti = T((double)st[i] + dd[i]);
+          if (i < NX ? k >= 1 : k < N) st_l = mr_max(st_l, mr_abs(sti));
+        }
       }
       for (int i = 0; i < NH; ++i) rbe.st(H[i], 0u, Rk + RCF::H + i);
       for (int i = 0; i < NZ; ++i) {
         rbe.st(T((double)g0[i] + dd[i]), 0u, Rk + RCF::G0 + i);
         rbe.st(g1[i], 0u, Rk + RCF::G1 + i);
+      }
+    }
+    if constexpr (refk) {
+      // S_k = S_k + Delta-S_{k-1} - Delta-S_k; U_k = u_k + p_{k+1} (U_0: + every w_j); lanes > N hold zeros
+      const T bprev = wprev(w, rs_b), pn0 = wnext(w, rs_p[0]), pn1 = wnext(w, rs_p[1]);
+      const T ws0 = wsum(w, rs_w[0]), ws1 = wsum(w, rs_w[1]);
+      if (own()) {
+        st_l = mr_max(st_l, mr_abs(rs_a + (k >= 1 ? bprev : T(0)) - rs_b));
+        if (k < N) {
+          st_l = mr_max(st_l, mr_abs(rs_u[0] + pn0 + (k == 0 ? ws0 : T(0))));
+          st_l = mr_max(st_l, mr_abs(rs_u[1] + pn1 + (k == 0 ? ws1 : T(0))));
+        }
       }
     }
 #if MR_PHASE_CYCLES
@@ -660,7 +692,7 @@ struct WaveSolver {
     fval = wsum(w, f_l);
     logs = wsum(w, lg_l);
     mi = wsum(w, mi_l);
-    me = NX * (N + 1);
+    me = refk ? 6 * N + 7 : NX * (N + 1);
     wsync(w);  // stage records visible to every lane before the Riccati sweep
 #if MR_PHASE_CYCLES
     if (trace) { tsub[2] += te1 - te0; tsub[3] += MR_CLOCK() - te1; }
@@ -1275,7 +1307,7 @@ struct WaveSolver {
         for (int a = 0; a < NU; ++a) accx += f.bw[a] * wbcast(w, acc, 32 + a);
         dxi = g0r ? accx : T(0);
         lds[lbase + lstep * k] = g0r ? accx : acc;
-        const bool dn = g1r & (k >= 1);
+        const bool dn = g1r & (k >= 1 || !MR_KKT_RESTATED);  // k = 0: the initial-state rows' multiplier step
         if constexpr (SSL) {
           if (dn) ss[(SSF::DNU + r) * WL + k] = acc;
         } else {  // branch-free: other lanes write stage k's record discard slot

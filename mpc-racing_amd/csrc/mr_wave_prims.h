@@ -74,6 +74,17 @@ __device__ __forceinline__ double wnext(const Wv&, double v) {
   return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
 }
 
+// value of lane (lane - 1) mod 64 (the previous stage's): v_mov_b32_dpp wave_ror:1
+__device__ __forceinline__ float wprev(const Wv&, float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x13C, 0xf, 0xf, false));
+}
+__device__ __forceinline__ double wprev(const Wv&, double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffLL), 0x13C, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x13C, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
 // value of lane src (src wave-uniform): v_readlane, result lands in an SGPR
 __device__ __forceinline__ int wbcast(const Wv&, int v, int src) { return __builtin_amdgcn_readlane(v, src); }
 __device__ __forceinline__ float wbcast(const Wv&, float v, int src) {
@@ -315,6 +326,8 @@ inline T wshfl(const Wv& w, T v, int src) {
 }
 template <typename T>
 inline T wnext(const Wv& w, T v) { return wshfl(w, v, (w.lane + 1) % WL); }
+template <typename T>
+inline T wprev(const Wv& w, T v) { return wshfl(w, v, (w.lane + WL - 1) % WL); }
 template <typename T>
 inline T wbcast(const Wv& w, T v, int src) { return wshfl(w, v, src); }
 template <typename T>

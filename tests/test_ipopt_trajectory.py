@@ -53,3 +53,30 @@ def test_iterates_match_dense_ipopt(name, i, K):
         np.testing.assert_allclose(tr[j, 1], mu, rtol=1e-12, err_msg=f"{name} {i} iteration {j}: mu")
     if name == "C3":
         assert max(row[4] for row in rows) > 1e3  # the inertia correction is exercised
+
+
+@pytest.mark.parametrize("i", [1, 10])
+def test_whole_solve_matches_dense_ipopt(i):
+    """Over a whole C2 solve (kinematic, tol 1e-8): the same optimality error at every iteration (IPOPT's
+    scaled stationarity / primal / complementarity measure on the reference's NLP, mr_solver.h
+    MR_KKT_RESTATED), hence the same barrier-parameter updates, the same termination iteration and the
+    same objective.  (Instance 1 ended one iteration later than IPOPT while the error was measured on the
+    restatement.)"""
+    from oracle.ipopt import solve_ipopt
+    from oracle.nlp import MPCProblem
+    cfg = wl.CONFIGS["C2"]
+    b = wl.make_batch("C2", limit=i + 1)
+    sub = {k: (v[..., i:i + 1].copy() if v is not None else None) for k, v in b.items()}
+    c = ht.config(cfg["N"], cfg["model"], "fp64", cfg["lane"], cfg["Ts"], tol=1e-8, acceptable_iter=15,
+                  acceptable_tol=1e-6)
+    o = ht.solve(c, sub, nthreads=1, scalar=True, trace_instance=0, trace_cap=520)
+    inst = wl.instance_dicts(b)[i]
+    p = MPCProblem(inst["state0"], inst["s0"], inst["cx"], inst["cy"], inst["max_error"], N=cfg["N"],
+                   Ts=cfg["Ts"], model=cfg["model"], lane_bounds=cfg["lane"])
+    r = solve_ipopt(p, tol=1e-8, max_iter=500, acceptable_tol=1e-6, acceptable_iter=15, log=True)
+    assert r.status == 0 and int(o["status"][0]) == 0
+    assert int(o["iters"][0]) == r.iters
+    for j, row in enumerate(r.log):
+        np.testing.assert_allclose(o["trace"][j, 0], row[1], rtol=1e-6, err_msg=f"iteration {j}: kkt")
+        np.testing.assert_allclose(o["trace"][j, 1], row[2], rtol=1e-12, err_msg=f"iteration {j}: mu")
+    np.testing.assert_allclose(o["obj"][0], r.obj, rtol=1e-10)
