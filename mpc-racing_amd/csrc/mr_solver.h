@@ -1642,7 +1642,8 @@ struct Solver {
       if (gphi < T(0)) {
         T t1 = g_ph * th / (-gphi);
         T t2 = delta_sw * th_pow / mr_exp(s_phi * mr_log(-gphi));
-        a_min = T(0.05) * mr_min(g_th, mr_min(t1, t2));
+        // IPOPT (W&B 2006 eq. 23, CalculateAlphaMin): the switching term only at theta <= theta_min
+        a_min = T(0.05) * mr_min(g_th, th <= theta_min ? mr_min(t1, t2) : t1);
       } else {
         a_min = T(0.05) * g_th;
       }

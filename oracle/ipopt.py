@@ -219,8 +219,10 @@ def _run(nlp, st, tol, max_iter, it0, filt, theta_max, theta_min, obj_scale, tra
         ph = fv - mu * float(np.log(s).sum())
         gphi = float(gf @ dz - mu * np.sum(ds / s))
         th_pow = th ** S_THETA
-        if gphi < 0:
-            a_min = 0.05 * min(G_TH, G_PH * th / (-gphi), DELTA_SW * th_pow / (-gphi) ** S_PHI)
+        if gphi < 0:  # W&B 2006 eq. 23: the switching term only at theta <= theta_min
+            a_min = 0.05 * min(G_TH, G_PH * th / (-gphi))
+            if th <= theta_min:
+                a_min = min(a_min, 0.05 * DELTA_SW * th_pow / (-gphi) ** S_PHI)
         else:
             a_min = 0.05 * G_TH
 
