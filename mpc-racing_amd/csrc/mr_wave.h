@@ -21,7 +21,6 @@
 //   nu[2][11][64] the dynamics rows' multipliers and their watchdog copy, fp64 in both precisions
 #pragma once
 #include <new>
-#include <type_traits>
 
 #include "mr_batch.h"
 #include "mr_wave_prims.h"
@@ -96,20 +95,12 @@ struct RCF {
     JUNK, NF                           // discard slot of the branch-free stores (any lane)
   };
 };
-#ifndef MR_PAIR
-#define MR_PAIR 0  // 1: inertia-correction trials factorised in pairs (riccati_pair, A/B option: slower); 0: one per pass
-#endif
-// MR_PAIR: the second chain's P, p0, p1, K, k0, k1 at RCF::OB (the layout of RCF::P .. RCF::K1 shifted by
-// AREA_SHIFT words)
-constexpr int RC_OB = 336;
-constexpr int AREA_SHIFT = RC_OB - RCF::P;
 #ifdef MR_RC_STRIDE_FORCE
 constexpr int RC_STRIDE = MR_RC_STRIDE_FORCE;  // A/B option (record footprint)
 #else
-constexpr int RC_STRIDE = MR_PAIR ? RC_OB + 128 : 336;  // words; 16-word (64 B) multiple
+constexpr int RC_STRIDE = 336;  // words; 16-word (64 B) multiple
 #endif
-static_assert(RCF::NF <= RC_OB, "record");
-static_assert(!MR_PAIR || RC_OB + (RCF::K1 + NU - RCF::P) <= RC_STRIDE, "second output area");
+static_assert(RCF::NF <= RC_STRIDE, "record");
 // Cold per-stage fields [f][64] after the records: touched only by the watchdog (its snapshot of the
 // iterate and the search direction) and the restoration phase (the relaxations p, n of the rows and
 // of the 6 vehicle dynamics rows, their bound duals and steps, the rows' equality multipliers y, the
@@ -150,8 +141,6 @@ struct WaveShared {
 constexpr int LDS_LD = 17;  // padded row of the 16 x 16 LDS tiles
 constexpr int LX_OFF = 0, LP_OFF = 16 * LDS_LD, LDX_OFF = 32 * LDS_LD;
 constexpr int LJUNK_OFF = LDX_OFF + WL * 12;  // one discard slot per lane (branch-free stores)
-constexpr int LPB_OFF = LDX_OFF;  // riccati_pair's second cost-to-go tile (the forward sweep's LDX rows are idle then)
-static_assert(LPB_OFF + 16 * LDS_LD <= LJUNK_OFF, "second tile");
 constexpr int LDS_WORDS = LJUNK_OFF + WL;
 
 // lower-triangular solves with L packed (00,10,11,20,21,22) as produced by chol3
@@ -271,7 +260,6 @@ struct WaveSolver {
   // rather than in the caller's private stack (a scratch round trip after every call)
   T res_ap, res_ad, res_gphi, res_alpha;
   int res_flags, res_nls, res_ntr, res_nsoc;
-  int rarea = 0;  // MR_PAIR: the record output area of the accepted factorisation (0: RCF::P.., 1: RC_OB..)
   double* trace = nullptr;
   int trace_cap = 0;
 #if MR_PHASE_CYCLES
@@ -392,11 +380,8 @@ struct WaveSolver {
         // du_N); zeros keep that step on defined values
         for (int q = 0; q < 48; ++q) Rk[RCF::J + q] = T(0);
         for (int q = 0; q < NX; ++q) Rk[RCF::C + q] = T(0);
-        for (int a = 0; a < (MR_PAIR ? 2 : 1); ++a) {  // both output areas
-          const int sh = a ? AREA_SHIFT : 0;
-          for (int q = 0; q < NU * NX; ++q) Rk[RCF::K + sh + q] = T(0);
-          for (int q = 0; q < NU; ++q) { Rk[RCF::K0 + sh + q] = T(0); Rk[RCF::K1 + sh + q] = T(0); }
-        }
+        for (int q = 0; q < NU * NX; ++q) Rk[RCF::K + q] = T(0);
+        for (int q = 0; q < NU; ++q) { Rk[RCF::K0 + q] = T(0); Rk[RCF::K1 + q] = T(0); }
       }
     }
     gmax = wmax(w, gmax);
@@ -997,223 +982,6 @@ struct WaveSolver {
     return true;
   }
 
-#if MR_PAIR
-  // ---------------- sweep 2 (original problem): two inertia-correction trials in one pass ----------------
-  // IPOPT's inertia correction tries delta = 0, then delta_1, delta_1 f, ... until the factorisation has
-  // the right inertia (every Q_uu pivot positive).  This sweep factorises two consecutive trials (da, db)
-  // of that sequence as two independent recursion chains that share the record gathers: chain A's
-  // cost-to-go tile at LP_OFF, chain B's in the (here idle) LDX region, chain A's P, p, K, k stored in the
-  // record's output slots, chain B's in the second output area (RCF::OB, same layout, +AREA_SHIFT words).
-  // Each chain does exactly the arithmetic of riccati<false> with its delta, so taking the first chain
-  // with the right inertia in sequence order gives IPOPT's iterates; the failed delta = 0 attempt (the
-  // norm on the blended model's indefinite Hessian) no longer costs a pass of its own.
-  // Returns bit 0: chain A has the right inertia, bit 1: chain B.
-  MR_SWEEP unsigned riccati_pair(T da, T db) {
-    MR_ASSUME_LDS_STATE();
-    const int l = ln, N = wu(w, this->N), g = l >> 4, c = l & 15;
-    const Wv w = this->w;
-    const WBuf<T> rb(rc, (unsigned)WL * (unsigned)RC_STRIDE);
-    MR_LDS T* const LT[2] = {lds + LP_OFF, lds + LPB_OFF};
-    const unsigned SH[2] = {0u, (unsigned)AREA_SHIFT};
-    auto R = [](int k) { return (unsigned)k * (unsigned)RC_STRIDE; };
-    for (int q = l; q < 16 * LDS_LD; q += WL) { LT[0][q] = T(0); LT[1][q] = T(0); }
-    wsync_lds(w);
-    FragPlan fp;
-    frag_plan(l, fp);
-    // LDS targets relative to each chain's tile (discard slots: the lane's absolute junk word)
-    int lq1[2][4], lq2[2][4];
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const bool j1 = fp.lp1[v] == LJUNK_OFF - LP_OFF + l, j2 = fp.lp2[v] == LJUNK_OFF - LP_OFF + l;
-      lq1[0][v] = fp.lp1[v];
-      lq2[0][v] = fp.lp2[v];
-      lq1[1][v] = j1 ? LJUNK_OFF - LPB_OFF + l : fp.lp1[v];
-      lq2[1][v] = j2 ? LJUNK_OFF - LPB_OFF + l : fp.lp2[v];
-    }
-    T dd[2][4];
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      dd[0][v] = ((fp.dlt >> v) & 1u) ? da : T(0);
-      dd[1][v] = ((fp.dlt >> v) & 1u) ? db : T(0);
-    }
-    const T sg[3] = {g == 0 ? T(1) : T(0), g == 1 ? T(1) : T(0), g == 2 ? T(1) : T(0)};
-    T raw_a[NGATHER], raw_b[NGATHER], raw_c[NGATHER];
-    frag_load(rb, R(N - 1), fp, raw_a);
-    frag_load(rb, R(N >= 2 ? N - 2 : 0), fp, raw_b);
-    {  // terminal cost-to-go of both chains: P_N = H_N,xx + delta I, p_N = g_N
-      const unsigned Rn = R(N);
-      const bool row = l < NX;
-      const int lr = row ? l : 0, jl = RCF::JUNK, jda = LJUNK_OFF - LP_OFF + l, jdb = LJUNK_OFF - LPB_OFF + l;
-      T hv[NX];
-#pragma unroll
-      for (int j = 0; j < NX; ++j) hv[j] = rb.ld(Rn, RCF::H + hidx(lr, j));
-      const T p0 = rb.ld(Rn, RCF::G0 + lr), p1 = rb.ld(Rn, RCF::G1 + lr);
-#pragma unroll
-      for (int j = 0; j < NX; ++j) {
-        const bool dj = l == j && delta_var(j);
-        const T va = hv[j] + (dj ? da : T(0)), vb = hv[j] + (dj ? db : T(0));
-        LT[0][row ? l * LDS_LD + j : jda] = va;
-        LT[1][row ? l * LDS_LD + j : jdb] = vb;
-        const bool st = row && j >= l;
-        rb.st(va, Rn, st ? RCF::P + pidx(lr, j) : jl);
-        rb.st(vb, Rn, st ? RCF::P + AREA_SHIFT + pidx(lr, j) : jl);
-      }
-      LT[0][row ? l * LDS_LD + 11 : jda] = p0;
-      LT[0][row ? l * LDS_LD + 12 : jda] = p1;
-      LT[1][row ? l * LDS_LD + 11 : jdb] = p0;
-      LT[1][row ? l * LDS_LD + 12 : jdb] = p1;
-      rb.st(p0, Rn, row ? RCF::PV0 + l : jl);
-      rb.st(p1, Rn, row ? RCF::PV1 + l : jl);
-      rb.st(p0, Rn, row ? RCF::PV0 + AREA_SHIFT + l : jl);
-      rb.st(p1, Rn, row ? RCF::PV1 + AREA_SHIFT + l : jl);
-    }
-    wsync_lds(w);
-    bool ok[2] = {true, true};
-    // One stage of NQ chains (q0 = the first chain's index), written phase by phase across the chains so
-    // the two independent dependency chains interleave in the instruction stream (one chain's MFMA /
-    // shuffle / rsq latencies are covered by the other's work).
-    auto stage = [&](auto NQc, int q0, int k, const T* raw_use, T* raw_fill) {
-      constexpr int NQ = decltype(NQc)::value;
-      const unsigned Rk = (unsigned)wu(w, (int)R(k));
-      MR_LDS T* LP[NQ];
-      T dq[NQ][4], dx[NQ][4], dx2[NQ][4], xb[NQ][4];
-      T eb[4];
-#pragma unroll
-      for (int s = 0; s < 4; ++s) eb[s] = raw_use[s];
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const int qq = NQ == 2 ? q : q0;
-        LP[q] = qq ? LT[1] : LT[0];
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          dq[q][v] = raw_use[4 + v] + (qq ? dd[1][v] : dd[0][v]);
-          dx[q][v] = dx2[q][v] = T(0);
-        }
-      }
-      frag_load(rb, (unsigned)wu(w, (int)R(k >= 2 ? k - 2 : 0)), fp, raw_fill);
-      // X = P^ E^
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        wmfma(w, LP[q][c * LDS_LD + g], eb[0], dx[q]);
-        wmfma(w, LP[q][c * LDS_LD + 8 + g], eb[2], dx2[q]);
-      }
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        wmfma(w, LP[q][c * LDS_LD + 4 + g], eb[1], dx[q]);
-        wmfma(w, LP[q][c * LDS_LD + 12 + g], eb[3], dx2[q]);
-      }
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-#pragma unroll
-        for (int v = 0; v < 4; ++v) xb[q][v] = dx[q][v] + dx2[q][v];
-        if constexpr (sizeof(T) == 4) wtranspose4(w, xb[q]);
-      }
-      // Q = (H + delta I | g0 | g1) + E^T X
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-#pragma unroll
-        for (int v = 0; v < 4; ++v) dx2[q][v] = T(0);
-        wmfma(w, eb[0], xb[q][0], dq[q]);
-        wmfma(w, eb[2], xb[q][2], dx2[q]);
-      }
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        wmfma(w, eb[1], xb[q][1], dq[q]);
-        wmfma(w, eb[3], xb[q][3], dx2[q]);
-      }
-#pragma unroll
-      for (int q = 0; q < NQ; ++q)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) dq[q][v] += dx2[q][v];
-      // Q_uu = L L^T, W = L^-1 Q_u., gains
-      T L[NQ][6], iv[NQ][3], w0[NQ][3], w1[NQ][3], wc[NQ][3], dw[NQ][4];
-      bool piv[NQ];
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        auto qat = [&](int a, int b) { return wbcast(w, dq[q][dreg(a)], dgrp(a) * 16 + b); };
-        T Rh[6] = {qat(11, 11), qat(11, 12), qat(11, 13), qat(12, 12), qat(12, 13), qat(13, 13)};
-        piv[q] = chol3r(Rh, L[q], iv[q]);
-        w0[q][0] = qat(11, 14); w0[q][1] = qat(12, 14); w0[q][2] = qat(13, 14);
-        w1[q][0] = qat(11, 15); w1[q][1] = qat(12, 15); w1[q][2] = qat(13, 15);
-        wc[q][0] = wshfl(w, dq[q][dreg(11)], dgrp(11) * 16 + c);
-        wc[q][1] = wshfl(w, dq[q][dreg(12)], dgrp(12) * 16 + c);
-        wc[q][2] = wshfl(w, dq[q][dreg(13)], dgrp(13) * 16 + c);
-      }
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        lsolve3r(L[q], iv[q], wc[q]);
-        const T wv = wc[q][0] * sg[0] + wc[q][1] * sg[1] + wc[q][2] * sg[2];
-#pragma unroll
-        for (int v = 0; v < 4; ++v) dw[q][v] = T(0);
-        wmfma(w, wv, wv, dw[q]);
-        lsolve3r(L[q], iv[q], w0[q]);
-        lsolve3r(L[q], iv[q], w1[q]);
-      }
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const int qq = NQ == 2 ? q : q0;
-        const unsigned sh = qq ? SH[1] : SH[0];
-        T kc[3] = {wc[q][0], wc[q][1], wc[q][2]};
-        ltsolve3r(L[q], iv[q], kc);
-        ltsolve3r(L[q], iv[q], w0[q]);
-        ltsolve3r(L[q], iv[q], w1[q]);
-        const bool kcol = (g == 0) & (c < NX), kf0 = (g == 0) & (c == NX), kf1 = (g == 0) & (c == NX + 1);
-#pragma unroll
-        for (int a = 0; a < NU; ++a) {
-          const unsigned idx = kcol ? RCF::K + sh + a * NX + c
-                                    : (kf0 ? RCF::K0 + sh + a : (kf1 ? RCF::K1 + sh + a : RCF::JUNK));
-          rb.st(kcol ? -kc[a] : (kf0 ? -w0[q][a] : -w1[q][a]), Rk, idx);
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const int qq = NQ == 2 ? q : q0;
-        const unsigned sh = qq ? SH[1] : SH[0];
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const T pv = dq[q][v] - dw[q][v];
-          const unsigned so = (unsigned)fp.st_p[v];
-          rb.st(pv, Rk, so == (unsigned)RCF::JUNK ? so : so + sh);
-          LP[q][qq ? lq1[1][v] : lq1[0][v]] = pv;
-          LP[q][qq ? lq2[1][v] : lq2[0][v]] = pv;
-        }
-        if (NQ == 2) ok[q] = piv[q] & ok[q];
-        else ok[q0] = piv[q] & ok[q0];
-      }
-      wsync_lds(w);
-    };
-    typedef std::integral_constant<int, 2> Two;
-    typedef std::integral_constant<int, 1> One;
-    int k = N - 1;
-    bool both = true;
-    for (;; k -= 3) {
-      stage(Two(), 0, k, raw_a, raw_c);
-      if (k == 0) break;
-      stage(Two(), 0, k - 1, raw_b, raw_a);
-      if (k == 1) break;
-      stage(Two(), 0, k - 2, raw_c, raw_b);
-      if (k == 2) break;
-      const bool a = wuni(w, ok[0]), b = wuni(w, ok[1]);
-      if (!a && !b) return 0u;
-      if (!(a && b)) { both = false; k -= 3; break; }
-    }
-    if (!both) {  // one chain failed: the other alone for the remaining stages (same prefetch rotation)
-      const int q0 = wuni(w, ok[0]) ? 0 : 1;
-      for (;; k -= 3) {
-        stage(One(), q0, k, raw_a, raw_c);
-        if (k == 0) break;
-        stage(One(), q0, k - 1, raw_b, raw_a);
-        if (k == 1) break;
-        stage(One(), q0, k - 2, raw_c, raw_b);
-        if (k == 2) break;
-        if (!wuni(w, ok[q0])) return 0u;
-      }
-    }
-    const unsigned m = (wuni(w, ok[0]) ? 1u : 0u) | (wuni(w, ok[1]) ? 2u : 0u);
-    if (m) wsync(w);
-    return m;
-  }
-#endif
 
   // ---------------- sweep 3: forward substitution, slack/dual steps ----------------
   //   Sequential part: per stage, three lane groups share one 11-term dot with dx_k (gathered from
@@ -1250,15 +1018,14 @@ struct WaveSolver {
       const bool g0r = (grp == 0) & (r < NX), g1r = (grp == 1) & (r < NX), g2r = (grp == 2) & (r < NU);
       const int r0 = g0r ? r : 0;
       int roff[NX], boff[NU], c0off, c1off;
-      const int ash = MR_PAIR && wu(w, rarea) ? AREA_SHIFT : 0;  // the accepted factorisation's output area
 #pragma unroll
       for (int j = 0; j < NX; ++j)
         roff[j] = g0r ? ehat_slot(r0, j, true)
-                      : (g1r ? RCF::P + ash + pidx(r, j) : (g2r ? RCF::K + ash + r * NX + j : RCF::CZERO));
+                      : (g1r ? RCF::P + pidx(r, j) : (g2r ? RCF::K + r * NX + j : RCF::CZERO));
 #pragma unroll
       for (int a = 0; a < NU; ++a) boff[a] = ehat_slot(r0, NX + a, g0r);
-      c0off = g0r ? ehat_slot(r0, 14, true) : (g1r ? RCF::PV0 + ash + r : (g2r ? RCF::K0 + ash + r : RCF::CZERO));
-      c1off = g1r ? RCF::PV1 + ash + r : (g2r ? RCF::K1 + ash + r : RCF::CZERO);
+      c0off = g0r ? ehat_slot(r0, 14, true) : (g1r ? RCF::PV0 + r : (g2r ? RCF::K0 + r : RCF::CZERO));
+      c1off = g1r ? RCF::PV1 + r : (g2r ? RCF::K1 + r : RCF::CZERO);
       static_assert(3 * WL <= LP_OFF + 16 * LDS_LD, "du staging");
       // LDS target of each lane's step result (branch-free, one store): group 0 dx_{k+1}[r] at
       // LDX[(k + 1) 12 + r] (row N + 1 <= 64; N = 63: the discard slots), group 2 du_k[r] at
@@ -1964,26 +1731,7 @@ struct WaveSolver {
       T delta = T(0);
       bool first = true, fact_ok = false;
       MR_T0();
-#if MR_PAIR
-      rarea = 0;
-      if (!rs) {
-        // the same trial sequence as below, two trials per pass: (0, d1), (d1 f, d1 f^2), ...
-        const T f = delta_last == T(0) ? T(100) : T(8);
-        T da = T(0), db = delta_last == T(0) ? T(1e-4) : mr_max(T(1e-20), delta_last / T(3));
-        for (int tries = 0; tries < 30; ++tries) {
-          MR_CNT(6);
-          const unsigned m = riccati_pair(da, db);
-          if (m & 1u) { delta = da; fact_ok = true; break; }
-          if ((m & 2u) && !(db > T(1e40))) { delta = db; rarea = 1; fact_ok = true; break; }
-          da = db * f;
-          db = da * f;
-          if (da > T(1e40)) break;
-        }
-      }
-      for (int tries = 0; rs && tries < 60; ++tries) {
-#else
       for (int tries = 0; tries < 60; ++tries) {
-#endif
         MR_CNT(6);
 #if MR_PHASE_CYCLES
         const unsigned long long tr0 = trace ? MR_CLOCK() : 0ull;

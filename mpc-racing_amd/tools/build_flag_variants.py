@@ -6,8 +6,7 @@ bounds of mpcracing.hip): variants/lib_<name>.so, run by tools/gpu_flags_ab.sh o
   slp      SLP vectorisation on (no -fno-slp-vectorize)
   w1       fp32 solve kernel at 1 wave per SIMD (MR_WAVES_PER_SIMD_F32=1, 512 VGPRs)
   ric3     Riccati operand gathers three stages ahead instead of two (MR_RIC_AHEAD=3)
-  nopair   one inertia-correction trial per Riccati pass (MR_PAIR=0, the round-2 scheme)
-  nopair464  nopair with the paired build's 464-word record stride (the footprint alone)
+  s464     a 464-word record stride (the footprint the rejected paired factorisation needed, git e417017)
   prio60   waves past iteration 60 raise their issue priority (s_setprio 3)
   cyc      per-sweep shader-cycle counters of the trace instance (tools/phase_probe.py)
 """
@@ -26,8 +25,7 @@ VARIANTS = {
     "slp": [f for f in DEFAULT_FLAGS if f != "-fno-slp-vectorize"],
     "w1": DEFAULT_FLAGS + ["-DMR_WAVES_PER_SIMD_F32=1"],
     "ric3": DEFAULT_FLAGS + ["-DMR_RIC_AHEAD=3"],
-    "nopair": DEFAULT_FLAGS + ["-DMR_PAIR=0"],
-    "nopair464": DEFAULT_FLAGS + ["-DMR_PAIR=0", "-DMR_RC_STRIDE_FORCE=464"],
+    "s464": DEFAULT_FLAGS + ["-DMR_RC_STRIDE_FORCE=464"],
     "prio60": DEFAULT_FLAGS + ["-DMR_PRIO_ITER=60"],
     "cyc": DEFAULT_FLAGS + ["-DMR_PHASE_CYCLES=1"],
 }
