@@ -752,12 +752,12 @@ struct WaveSolver {
       const int a_ = a < NZ ? a : 0;
       fp.off[4 + v] = a < NZ ? (c < NZ ? RCF::H + hidx(a_, c) : (c == 14 ? RCF::G0 + a_ : RCF::G1 + a_)) : RCF::CZERO;
       if (a < NZ && a == c && delta_var(a)) fp.dlt |= 1u << v;
-      // outputs of D register v: packed-upper P | p0 | p1, LDS image of P^
+      // outputs of D register v: packed-upper P | p (= p0 + mu p1, column 14), LDS image of P^
       const int junk_r = RCF::JUNK, junk_l = LJUNK_OFF - LP_OFF + lane;  // lp* index from LP
       const bool ax = a < NX, up = ax & (c < NX) & (a <= c);
-      const bool c14 = ax & (c == 14), c15 = ax & (c == 15);
-      fp.st_p[v] = up ? RCF::P + pidx(a, c) : (c14 ? RCF::PV0 + a : (c15 ? RCF::PV1 + a : junk_r));
-      fp.lp1[v] = up ? a * LDS_LD + c : (c14 ? a * LDS_LD + 11 : (c15 ? a * LDS_LD + 12 : junk_l));
+      const bool c14 = ax & (c == 14);
+      fp.st_p[v] = up ? RCF::P + pidx(a, c) : (c14 ? RCF::PV0 + a : junk_r);
+      fp.lp1[v] = up ? a * LDS_LD + c : (c14 ? a * LDS_LD + 11 : junk_l);
       fp.lp2[v] = up ? c * LDS_LD + a : fp.lp1[v];
     }
   }
@@ -774,12 +774,16 @@ struct WaveSolver {
   }
 
   // ---------------- sweep 2: Riccati factorisation on the matrix cores ----------------
-  // Backward over stages, with P^ = [P' | p0' | p1'] (cost-to-go of stage k+1) kept in LDS:
-  //   X    = P^ E^                        4 x v_mfma 16x16x4  (= [P'A  P'B | P'c + p0' | p1'])
-  //   Q    = (H + dI | g0 | g1) + E^T X   4 x v_mfma          (E^'s B fragment is E^T's A fragment)
+  // Backward over stages, with P^ = [P' | p'] (cost-to-go of stage k+1) kept in LDS:
+  //   X    = P^ E^                        3 x v_mfma 16x16x4  (= [P'A  P'B | P'c + p'])
+  //   Q    = (H + dI | g) + E^T X         3 x v_mfma          (E^'s B fragment is E^T's A fragment)
   //   Q_uu = L L^T (3x3, wave-uniform),   W = L^{-1} Q_u.     (one column per lane)
   //   P^   = Q_x. - W^T W                 1 x v_mfma          (upper triangle mirrored)
-  //   K = -L^{-T} W_x,  k0 | k1 = -L^{-T} w0 | w1
+  //   K = -L^{-T} W_x,  k = -L^{-T} w
+  // The right-hand side is the iteration's: g = g0 + mu g1 (the evaluation sweep stores the barrier
+  // gradient's mu-free and mu parts because mu is updated after it; the gathered g1 column is folded into
+  // the g0 column by a DPP row shift), so P^ has one vector column and E^'s contraction index one row less:
+  // the fourth K-chunk of both products is zero and skipped (7 MFMAs per stage instead of 9).
   // Stage k-2's record is gathered (8 loads per lane) while stage k is factorised.  The record gets
   // P, p0, p1, K, k0, k1 of stage k; the forward recursion forms A dx + B du + c from the stage's
   // Jacobian itself (no closed-loop map is stored: 132 fewer words written per stage and
@@ -790,7 +794,7 @@ struct WaveSolver {
   // tile), then P^ -= Y^T Y entry-wise.  False if M is not positive definite.
   // In fp64 whatever T (mr_solver.h noise_cond: the vehicle block of P^ is otherwise fp32 rounding noise
   // where a relaxation is active); the L^-1 columns go through the LX scratch tile as doubles.
-  MR_HD bool noise_tile(int k, MR_LDS T* LP) const {
+  MR_HD bool noise_tile(int k, MR_LDS T* LP, T mu) const {
     typedef double D;
     static_assert(6 * 16 * sizeof(D) <= 16 * LDS_LD * sizeof(T), "LX scratch holds 6 x 16 doubles");
     MR_LDS D* const LX = (MR_LDS D*)(lds + LX_OFF);
@@ -808,7 +812,7 @@ struct WaveSolver {
     if (!wuni(w, ok)) return false;
     const int c = l < 13 ? l : 0;
     D col[6];
-    for (int i = 0; i < 6; ++i) col[i] = (D)LP[i * LDS_LD + c] + (c == 11 ? gw0[i] : (c == 12 ? gw1[i] : 0.0));
+    for (int i = 0; i < 6; ++i) col[i] = (D)LP[i * LDS_LD + c] + (c == 11 ? gw0[i] + (D)mu * gw1[i] : 0.0);
     lsolve6(L, col);
     if (l < 13)
       for (int a = 0; a < 6; ++a) LX[a * 16 + l] = col[a];
@@ -824,7 +828,7 @@ struct WaveSolver {
   }
 
   template <bool RESTO>
-  MR_SWEEP bool riccati(T delta, T /*mu*/) {
+  MR_SWEEP bool riccati(T delta, T mu) {
     MR_ASSUME_LDS_STATE();
     const int l = ln, N = wu(w, this->N), g = l >> 4, c = l & 15;
     const Wv w = this->w;
@@ -843,6 +847,7 @@ struct WaveSolver {
     // lane-constant 0/1 selectors: per-lane picks as products (exact for finite values), so the
     // step has no lane-divergent branches
     const T sg[3] = {g == 0 ? T(1) : T(0), g == 1 ? T(1) : T(0), g == 2 ? T(1) : T(0)};
+    const T s14 = c == 14 ? mu : T(0), k15 = c == 15 ? T(0) : T(1);  // g = g0 + mu g1 into column 14
     // operand gathers run two stages ahead of the factorisation (three rotating buffers): a record
     // gather is an Infinity-Cache / HBM round trip (the 8 192 instances' records do not fit the L2),
     // longer than one stage's arithmetic
@@ -869,21 +874,22 @@ struct WaveSolver {
         LP[row ? l * LDS_LD + j : jd] = v;
         rb.st(v, Rn, (row && j >= l) ? RCF::P + pidx(lr, j) : jl);
       }
-      LP[row ? l * LDS_LD + 11 : jd] = p0;
-      LP[row ? l * LDS_LD + 12 : jd] = p1;
-      rb.st(p0, Rn, row ? RCF::PV0 + l : jl);
-      rb.st(p1, Rn, row ? RCF::PV1 + l : jl);
+      const T pN = p0 + mu * p1;
+      LP[row ? l * LDS_LD + 11 : jd] = pN;
+      rb.st(pN, Rn, row ? RCF::PV0 + l : jl);
     }
     wsync_lds(w);
     // one stage; the loop below is unrolled by three so the prefetch buffers rotate roles
     // (no register copies of in-flight loads, hence exact vmcnt waits instead of vmcnt(0))
     auto step = [&](int k, const T* raw_use, T* raw_fill) -> bool {
       bool noise_ok = true;
-      if constexpr (RESTO) noise_ok = noise_tile(k, LP);  // P^ of stage k+1 minimised over the disturbance
+      if constexpr (RESTO) noise_ok = noise_tile(k, LP, mu);  // P^ of stage k+1 minimised over the disturbance
       // stage offsets as visibly wave-uniform values (SGPR soffsets, not per-lane waterfall loops)
       const unsigned Rk = (unsigned)wu(w, (int)R(k));
       T eb[4], dq[4];
       frag_finish(dd, raw_use, eb, dq);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) dq[v] = (dq[v] + s14 * wrow_next(w, dq[v])) * k15;  // g0 + mu g1 | 0
       frag_load(rb, (unsigned)wu(w, (int)R(k >= MR_RIC_AHEAD ? k - MR_RIC_AHEAD : 0)), fp, raw_fill);  // unconditional: k < AHEAD re-read stage 0's record
       // X = P^ E^  (A fragment s: P^[c][4s+g])
       // two independent 2-MFMA accumulation chains (k = 0..7 | 8..15) instead of one 4-long
@@ -891,8 +897,7 @@ struct WaveSolver {
       T dx[4] = {T(0), T(0), T(0), T(0)}, dx2[4] = {T(0), T(0), T(0), T(0)};
       wmfma(w, LP[c * LDS_LD + g], eb[0], dx);
       wmfma(w, LP[c * LDS_LD + 8 + g], eb[2], dx2);
-      wmfma(w, LP[c * LDS_LD + 4 + g], eb[1], dx);
-      wmfma(w, LP[c * LDS_LD + 12 + g], eb[3], dx2);
+      wmfma(w, LP[c * LDS_LD + 4 + g], eb[1], dx);  // (K-chunk 12..15 is zero)
 #pragma unroll
       for (int v = 0; v < 4; ++v) dx[v] += dx2[v];
       // B fragments X[4s+g][c]
@@ -905,8 +910,7 @@ struct WaveSolver {
         T dq2[4] = {T(0), T(0), T(0), T(0)};
         wmfma(w, eb[0], xb[0], dq);
         wmfma(w, eb[2], xb[2], dq2);
-        wmfma(w, eb[1], xb[1], dq);
-        wmfma(w, eb[3], xb[3], dq2);
+        wmfma(w, eb[1], xb[1], dq);  // (K-chunk 12..15 is zero)
 #pragma unroll
         for (int v = 0; v < 4; ++v) dq[v] += dq2[v];
       }
@@ -915,28 +919,25 @@ struct WaveSolver {
       T L[6], iv[3];
       const bool piv_ok = chol3r(Rh, L, iv);  // checked every second stage (below)
       T w0[3] = {qat(11, 14), qat(12, 14), qat(13, 14)};
-      T w1[3] = {qat(11, 15), qat(12, 15), qat(13, 15)};
       lsolve3r(L, iv, w0);
-      lsolve3r(L, iv, w1);
       T wc[3] = {wshfl(w, dq[dreg(11)], dgrp(11) * 16 + c), wshfl(w, dq[dreg(12)], dgrp(12) * 16 + c),
                  wshfl(w, dq[dreg(13)], dgrp(13) * 16 + c)};
       lsolve3r(L, iv, wc);  // W[:, c]
       const T wv = wc[0] * sg[0] + wc[1] * sg[1] + wc[2] * sg[2];  // W[g][c] (0 for g = 3)
       T dw[4] = {T(0), T(0), T(0), T(0)};
       wmfma(w, wv, wv, dw);  // W^T W
-      // gains: K[:, c] = -L^{-T} W[:, c], feed-forward k0, k1
-      T kc[3] = {wc[0], wc[1], wc[2]}, k0[3] = {w0[0], w0[1], w0[2]}, k1[3] = {w1[0], w1[1], w1[2]};
+      // gains: K[:, c] = -L^{-T} W[:, c], feed-forward k
+      T kc[3] = {wc[0], wc[1], wc[2]}, k0[3] = {w0[0], w0[1], w0[2]};
       ltsolve3r(L, iv, kc);
       ltsolve3r(L, iv, k0);
-      ltsolve3r(L, iv, k1);
       {  // branch-free gain stores (other lanes hit the discard slot): a loop free of divergent
          // branches keeps the waits for the prefetched operands exact across the back-edge
-        // row a of K by lanes (0, c < 11), k0[a] by lane (0, 11), k1[a] by lane (0, 12): one store per a
-        const bool kcol = (g == 0) & (c < NX), kf0 = (g == 0) & (c == NX), kf1 = (g == 0) & (c == NX + 1);
+        // row a of K by lanes (0, c < 11), k[a] by lane (0, 11): one store per a
+        const bool kcol = (g == 0) & (c < NX), kf0 = (g == 0) & (c == NX);
 #pragma unroll
         for (int a = 0; a < NU; ++a) {
-          const unsigned idx = kcol ? RCF::K + a * NX + c : (kf0 ? RCF::K0 + a : (kf1 ? RCF::K1 + a : RCF::JUNK));
-          rb.st(kcol ? -kc[a] : (kf0 ? -k0[a] : -k1[a]), Rk, idx);
+          const unsigned idx = kcol ? RCF::K + a * NX + c : (kf0 ? RCF::K0 + a : RCF::JUNK);
+          rb.st(kcol ? -kc[a] : -k0[a], Rk, idx);
         }
       }
 #pragma unroll
@@ -1025,7 +1026,7 @@ struct WaveSolver {
 #pragma unroll
       for (int a = 0; a < NU; ++a) boff[a] = ehat_slot(r0, NX + a, g0r);
       c0off = g0r ? ehat_slot(r0, 14, true) : (g1r ? RCF::PV0 + r : (g2r ? RCF::K0 + r : RCF::CZERO));
-      c1off = g1r ? RCF::PV1 + r : (g2r ? RCF::K1 + r : RCF::CZERO);
+      c1off = RCF::CZERO;  // (the Riccati's p and k already carry mu)
       static_assert(3 * WL <= LP_OFF + 16 * LDS_LD, "du staging");
       // LDS target of each lane's step result (branch-free, one store): group 0 dx_{k+1}[r] at
       // LDX[(k + 1) 12 + r] (row N + 1 <= 64; N = 63: the discard slots), group 2 du_k[r] at
@@ -1174,7 +1175,7 @@ struct WaveSolver {
       T du[NU] = {T(0), T(0), T(0)};
       if (k < N)
         for (int a = 0; a < NU; ++a) {
-          T v = Rk[RCF::K0 + a] + mu * Rk[RCF::K1 + a];
+          T v = Rk[RCF::K0 + a];  // k = k0 + mu k1 (riccati)
           for (int j = 0; j < NX; ++j) v += Rk[RCF::K + a * NX + j] * dx[j];
           du[a] = v;
         }
@@ -1193,7 +1194,7 @@ struct WaveSolver {
       T Pn[NP], sw[6], rhs[6], wv[6];
       for (int i = 0; i < NP; ++i) Pn[i] = Rn[RCF::P + i];
       for (int i = 0; i < 6; ++i) {
-        T v = Rn[RCF::PV0 + i] + mu * Rn[RCF::PV1 + i];
+        T v = Rn[RCF::PV0 + i];  // p = p0 + mu p1 (riccati)
         for (int l = 0; l < NX; ++l) v += Pn[pidx(i, l)] * dx[l];
         rhs[i] = v + cb[(CSF::CGW0 + i) * WL + k] + mu * cb[(CSF::CGW1 + i) * WL + k];
         sw[i] = cb[(CSF::CSW + i) * WL + k];
@@ -1205,7 +1206,7 @@ struct WaveSolver {
       // multiplier step dnu_{k+1} = P_{k+1} dx_{k+1} + p_{k+1} (correction form, eval_sweep)
       if (ln == k + 1)
         for (int i = 0; i < NX; ++i) {
-          T v = Rn[RCF::PV0 + i] + mu * Rn[RCF::PV1 + i];
+          T v = Rn[RCF::PV0 + i];  // p = p0 + mu p1 (riccati)
           for (int l = 0; l < NX; ++l) v += Pn[pidx(i, l)] * dx[l];
           S(SSF::DNU + i) = v;  // correction form: the multiplier step itself
         }

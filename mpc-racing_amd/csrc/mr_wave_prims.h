@@ -74,6 +74,16 @@ __device__ __forceinline__ double wnext(const Wv&, double v) {
   return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
 }
 
+// value of lane + 1 within the lane's row of 16 (0 for the row's last lane): v_mov_b32_dpp row_shl:1
+__device__ __forceinline__ float wrow_next(const Wv&, float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x101, 0xf, 0xf, true));
+}
+__device__ __forceinline__ double wrow_next(const Wv&, double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffLL), 0x101, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x101, 0xf, 0xf, true);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
 // value of lane (lane - 1) mod 64 (the previous stage's): v_mov_b32_dpp wave_ror:1
 __device__ __forceinline__ float wprev(const Wv&, float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x13C, 0xf, 0xf, false));
@@ -328,6 +338,11 @@ template <typename T>
 inline T wnext(const Wv& w, T v) { return wshfl(w, v, (w.lane + 1) % WL); }
 template <typename T>
 inline T wprev(const Wv& w, T v) { return wshfl(w, v, (w.lane + WL - 1) % WL); }
+template <typename T>
+inline T wrow_next(const Wv& w, T v) {
+  const T r = wshfl(w, v, (w.lane & 15) < 15 ? w.lane + 1 : w.lane);
+  return (w.lane & 15) < 15 ? r : T(0);
+}
 template <typename T>
 inline T wbcast(const Wv& w, T v, int src) { return wshfl(w, v, src); }
 template <typename T>
