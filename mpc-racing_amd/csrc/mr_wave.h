@@ -89,16 +89,15 @@ struct SSF {
 struct RCF {
   enum {
     J = 0, C = J + 48, H = C + NX, G0 = H + NH, G1 = G0 + NZ,
-    P = G1 + NZ, PV0 = P + NP,
-    PV1 = PV0 + NX, K = PV1 + NX, K0 = K + NU * NX, K1 = K0 + NU,
-    CONE = K1 + NU, CZERO, SELP, SEL0,  // constants 1, 0, [k > 0], [k == 0] (written once per solve)
+    P = G1 + NZ, PV0 = P + NP, K = PV0 + NX, K0 = K + NU * NX,
+    CONE = K0 + NU, CZERO, SELP, SEL0,  // constants 1, 0, [k > 0], [k == 0] (written once per solve)
     JUNK, NF                           // discard slot of the branch-free stores (any lane)
   };
 };
 #ifdef MR_RC_STRIDE_FORCE
 constexpr int RC_STRIDE = MR_RC_STRIDE_FORCE;  // A/B option (record footprint)
 #else
-constexpr int RC_STRIDE = 336;  // words; 16-word (64 B) multiple
+constexpr int RC_STRIDE = (RCF::NF + 15) / 16 * 16;  // words; 16-word (64 B) multiple (320)
 #endif
 static_assert(RCF::NF <= RC_STRIDE, "record");
 // Cold per-stage fields [f][64] after the records: touched only by the watchdog (its snapshot of the
@@ -375,13 +374,13 @@ struct WaveSolver {
       Rk[RCF::SEL0] = k > 0 ? T(0) : T(1);
       if (k == N) {
         // stage N has no dynamics and no gains: the evaluation and Riccati sweeps never write its
-        // Jacobian / defect / K / k0 / k1 slots, yet the forward recursion's last step (k = N) gathers
+        // Jacobian / defect / K / k slots, yet the forward recursion's last step (k = N) gathers
         // them in its lane groups 0 and 2 (whose results go only to the unused LDX row N + 1 and
         // du_N); zeros keep that step on defined values
         for (int q = 0; q < 48; ++q) Rk[RCF::J + q] = T(0);
         for (int q = 0; q < NX; ++q) Rk[RCF::C + q] = T(0);
         for (int q = 0; q < NU * NX; ++q) Rk[RCF::K + q] = T(0);
-        for (int q = 0; q < NU; ++q) { Rk[RCF::K0 + q] = T(0); Rk[RCF::K1 + q] = T(0); }
+        for (int q = 0; q < NU; ++q) Rk[RCF::K0 + q] = T(0);
       }
     }
     gmax = wmax(w, gmax);
@@ -725,7 +724,7 @@ struct WaveSolver {
   struct FragPlan {
     int off[NGATHER];  // record offsets: data entries, or the record's constant slots (CONE, CZERO, SELP, SEL0)
     unsigned dlt;  // D registers on the diagonal of H (+ delta)
-    int st_p[4], lp1[4], lp2[4];  // per D register: record / LDS targets (discard slots if none)
+    int st_p[4], lp[4];  // per D register: record / LDS targets (discard slots if none)
   };
   // record slot of entry (i, j) of E^ (either stage class k = 0 / k > 0): its data word, or the
   // constant slot holding its value; CZERO when !keep
@@ -752,13 +751,13 @@ struct WaveSolver {
       const int a_ = a < NZ ? a : 0;
       fp.off[4 + v] = a < NZ ? (c < NZ ? RCF::H + hidx(a_, c) : (c == 14 ? RCF::G0 + a_ : RCF::G1 + a_)) : RCF::CZERO;
       if (a < NZ && a == c && delta_var(a)) fp.dlt |= 1u << v;
-      // outputs of D register v: packed-upper P | p (= p0 + mu p1, column 14), LDS image of P^
-      const int junk_r = RCF::JUNK, junk_l = LJUNK_OFF - LP_OFF + lane;  // lp* index from LP
-      const bool ax = a < NX, up = ax & (c < NX) & (a <= c);
+      // outputs of D register v: packed-upper P | p (column 14) to the record; the whole tile of P^
+      // (both triangles as the product computes them, one LDS write per register) to LDS
+      const int junk_r = RCF::JUNK, junk_l = LJUNK_OFF - LP_OFF + lane;  // lp index from LP
+      const bool ax = a < NX, sq = ax & (c < NX), up = sq & (a <= c);
       const bool c14 = ax & (c == 14);
       fp.st_p[v] = up ? RCF::P + pidx(a, c) : (c14 ? RCF::PV0 + a : junk_r);
-      fp.lp1[v] = up ? a * LDS_LD + c : (c14 ? a * LDS_LD + 11 : junk_l);
-      fp.lp2[v] = up ? c * LDS_LD + a : fp.lp1[v];
+      fp.lp[v] = sq ? a * LDS_LD + c : (c14 ? a * LDS_LD + 11 : junk_l);
     }
   }
   static MR_HD void frag_load(const WBuf<T>& rb, unsigned ro, const FragPlan& fp, T* raw) {
@@ -778,14 +777,14 @@ struct WaveSolver {
   //   X    = P^ E^                        3 x v_mfma 16x16x4  (= [P'A  P'B | P'c + p'])
   //   Q    = (H + dI | g) + E^T X         3 x v_mfma          (E^'s B fragment is E^T's A fragment)
   //   Q_uu = L L^T (3x3, wave-uniform),   W = L^{-1} Q_u.     (one column per lane)
-  //   P^   = Q_x. - W^T W                 1 x v_mfma          (upper triangle mirrored)
+  //   P^   = Q_x. - W^T W                 1 x v_mfma
   //   K = -L^{-T} W_x,  k = -L^{-T} w
   // The right-hand side is the iteration's: g = g0 + mu g1 (the evaluation sweep stores the barrier
   // gradient's mu-free and mu parts because mu is updated after it; the gathered g1 column is folded into
   // the g0 column by a DPP row shift), so P^ has one vector column and E^'s contraction index one row less:
   // the fourth K-chunk of both products is zero and skipped (7 MFMAs per stage instead of 9).
   // Stage k-2's record is gathered (8 loads per lane) while stage k is factorised.  The record gets
-  // P, p0, p1, K, k0, k1 of stage k; the forward recursion forms A dx + B du + c from the stage's
+  // P, p, K, k of stage k; the forward recursion forms A dx + B du + c from the stage's
   // Jacobian itself (no closed-loop map is stored: 132 fewer words written per stage and
   // factorisation, and a smaller record).
   // Restoration phase: the cost-to-go tile P^ of stage k+1 (LP) minimised over the disturbance of
@@ -944,8 +943,7 @@ struct WaveSolver {
       for (int v = 0; v < 4; ++v) {  // branch-free: lanes without a target write their discard slot
         const T pv = dq[v] - dw[v];
         rb.st(pv, Rk, (unsigned)fp.st_p[v]);
-        LP[fp.lp1[v]] = pv;
-        LP[fp.lp2[v]] = pv;
+        LP[fp.lp[v]] = pv;
       }
       wsync_lds(w);
       return piv_ok & noise_ok;
@@ -987,7 +985,7 @@ struct WaveSolver {
   // ---------------- sweep 3: forward substitution, slack/dual steps ----------------
   //   Sequential part: per stage, three lane groups share one 11-term dot with dx_k (gathered from
   //   lanes 0..10): [A | c] rows -> A dx_k + c, P_k rows -> the costate step, K_k rows -> du_k =
-  //   K_k dx_k + k0 + mu k1; then dx_{k+1} = A dx_k + c + B du_k (stage Jacobian from the record,
+  //   K_k dx_k + k; then dx_{k+1} = A dx_k + c + B du_k (stage Jacobian from the record,
   //   no closed-loop map).  Then stage-parallel: slack / multiplier steps and the step limits.
   MR_SWEEP void forward(T& ap, T& ad, T& gphi) {
     MR_UNIFORM_P();
@@ -1010,7 +1008,7 @@ struct WaveSolver {
       // row . dx_k (dx_k gathered from lanes 0..10): group 0 (lanes 0..10) row i of [A | c] of the
       // stage map E^ -> (A dx_k + c)[i]; group 1 (lanes 16..26) row i of P_k -> the costate step
       // dnu_k[i] = P_k dx_k + p_k - nu_k (k >= 1); group 2 (lanes 32..34) row a of K_k ->
-      // du_k[a] = K_k dx_k + k0 + mu k1.  Then group 0 adds B du_k (du_k read from group 2):
+      // du_k[a] = K_k dx_k + k.  Then group 0 adds B du_k (du_k read from group 2):
       // dx_{k+1} = A dx_k + B du_k + c.  Every lane gathers its row from stage k's record (one
       // record, a few cache lines per load), instead of each lane reading its own stage's P and K
       // afterwards (a different cache line per lane and load).  Lanes without a row read the
@@ -1018,7 +1016,7 @@ struct WaveSolver {
       const int grp = ln >> 4, r = ln & 15;
       const bool g0r = (grp == 0) & (r < NX), g1r = (grp == 1) & (r < NX), g2r = (grp == 2) & (r < NU);
       const int r0 = g0r ? r : 0;
-      int roff[NX], boff[NU], c0off, c1off;
+      int roff[NX], boff[NU], c0off;
 #pragma unroll
       for (int j = 0; j < NX; ++j)
         roff[j] = g0r ? ehat_slot(r0, j, true)
@@ -1026,7 +1024,6 @@ struct WaveSolver {
 #pragma unroll
       for (int a = 0; a < NU; ++a) boff[a] = ehat_slot(r0, NX + a, g0r);
       c0off = g0r ? ehat_slot(r0, 14, true) : (g1r ? RCF::PV0 + r : (g2r ? RCF::K0 + r : RCF::CZERO));
-      c1off = RCF::CZERO;  // (the Riccati's p and k already carry mu)
       static_assert(3 * WL <= LP_OFF + 16 * LDS_LD, "du staging");
       // LDS target of each lane's step result (branch-free, one store): group 0 dx_{k+1}[r] at
       // LDX[(k + 1) 12 + r] (row N + 1 <= 64; N = 63: the discard slots), group 2 du_k[r] at
@@ -1039,7 +1036,7 @@ struct WaveSolver {
       // with one exit test per step at its end (uniform control, no copies of in-flight loads): the
       // waits for a set are exact vmcnt counts, not drains at the loop head.
       struct FwdRow {
-        T rw[NX], bw[NU], c0, c1;
+        T rw[NX], bw[NU], c0;  // (the Riccati's p and k already carry mu)
       };
       auto fload = [&](int kk, FwdRow& f) {
         kk = kk < N ? kk : N;
@@ -1049,14 +1046,13 @@ struct WaveSolver {
 #pragma unroll
         for (int a = 0; a < NU; ++a) f.bw[a] = wb.ld(ro, (unsigned)boff[a]);
         f.c0 = wb.ld(ro, (unsigned)c0off);
-        f.c1 = wb.ld(ro, (unsigned)c1off);
       };
       auto fstep = [&](int k, const FwdRow& f) {
         T dxv[NX];
         wgather<T, NX>(w, dxi, dxv);
 #if MR_FWD_TREE
         // the 11-term dot as three interleaved chains (critical path 4 FMAs + 2 adds, not 11)
-        T a0 = f.c0 + mu * f.c1, a1 = f.rw[1] * dxv[1], a2 = f.rw[2] * dxv[2];
+        T a0 = f.c0, a1 = f.rw[1] * dxv[1], a2 = f.rw[2] * dxv[2];
         a0 += f.rw[0] * dxv[0];
 #pragma unroll
         for (int j = 3; j < NX; j += 3) {
@@ -1066,7 +1062,7 @@ struct WaveSolver {
         }
         const T acc = (a0 + a1) + a2;
 #else
-        T acc = f.c0 + mu * f.c1;
+        T acc = f.c0;
         for (int j = 0; j < NX; ++j) acc += f.rw[j] * dxv[j];
 #endif
         // dx_{k+1} = (A dx_k + c) + B du_k on group 0, du_k from group 2 (lanes 32..34)
@@ -1175,7 +1171,7 @@ struct WaveSolver {
       T du[NU] = {T(0), T(0), T(0)};
       if (k < N)
         for (int a = 0; a < NU; ++a) {
-          T v = Rk[RCF::K0 + a];  // k = k0 + mu k1 (riccati)
+          T v = Rk[RCF::K0 + a];  // k (the Riccati's, mu already in)
           for (int j = 0; j < NX; ++j) v += Rk[RCF::K + a * NX + j] * dx[j];
           du[a] = v;
         }
