@@ -194,6 +194,34 @@ def _lib_sha():
     return h.hexdigest()[:16]
 
 
+def pipelined(args, solver, dev_in, out, batch, B, dev, local, nstreams):
+    """Serving-mode figure, reported beside the line's value (which times one batch at a time): the same
+    batch on ``nstreams`` independent handles (own workspaces) and HIP streams, 2 x steps launches
+    round-robin, so one batch's bulk runs on the CUs the previous batch's few long solves leave idle.
+    Each launch solves the whole batch (results checked identical to the timed leg's)."""
+    import torch
+    from mpcracing.batch import solver_for_config
+    hs = [solver] + [solver_for_config(args.config, B, device=local, dispatch_order=args.dispatch_order)
+                     for _ in range(nstreams - 1)]
+    ins = [dev_in] + [h.to_device(batch) for h in hs[1:]]
+    outs = [h.alloc_outputs(B) for h in hs]
+    streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
+    for h, i, o, st in zip(hs, ins, outs, streams):
+        h.launch(i, o, st)
+    torch.cuda.synchronize(dev)
+    n = 2 * args.steps
+    t0 = time.perf_counter()
+    for q in range(n):
+        j = q % nstreams
+        hs[j].launch(ins[j], outs[j], streams[j])
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    same = all(bool(torch.equal(o[k], out[k])) for o in outs for k in ("status", "iters", "obj"))
+    return {"streams": nstreams, "launches": n, "value": B * n / el, "unit": "solves/s",
+            "ms_per_batch": el / n * 1e3, "results_identical": same,
+            "note": "independent batches in flight on separate streams (not the line's value)"}
+
+
 def cpu_check(args, rank, world):
     """--cpu-check: the multi-rank plumbing without a GPU (gloo): each rank builds its shard and the
     counters go through reduce_counters; rank 0 prints the shard layout.  Used by tests/test_multirank.py."""
@@ -229,9 +257,12 @@ def main():
     ap.add_argument("--per-gpu", type=int, default=None)
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-latency", action="store_true", help="skip the B = 1 latency probe (profiling runs)")
+    ap.add_argument("--no-latency", action="store_true", help="skip the B = 1 latency probe and the pipelined figure (profiling runs: "
+                                                           "only the timed launches)")
     ap.add_argument("--cpu-check", action="store_true", help="multi-rank plumbing on CPU (gloo), no solve")
     ap.add_argument("--dispatch-order", type=int, default=1, help="mr_config.dispatch_order (A/B runs)")
+    ap.add_argument("--pipeline", type=int, default=4,
+                    help="streams of the serving-mode figure 'pipelined' (< 2: skip it)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU test of the rank plumbing of the real path (MR_BENCH_BACKEND=gloo): process group, "
                          "shards, counter reduction and the JSON line, with the solves skipped (no GPU)")
@@ -330,6 +361,10 @@ def main():
             lat.append(time.perf_counter() - t)
         lat_b1_ms = float(np.median(lat[1:]) * 1e3)
 
+    pipe = None
+    if args.pipeline >= 2 and world == 1 and not dry and not args.no_latency:
+        pipe = pipelined(args, solver, dev_in, out, batch, B, dev, local, args.pipeline)
+
     tot, elapsed_max = reduce_counters(
         torch.tensor([B * args.steps, iters_launch, alg_bytes, B] + stc.tolist(), dtype=torch.float64, device=dev),
         elapsed, world)
@@ -383,6 +418,8 @@ def main():
                          "copy_source": "measured in this run: 1 GiB fp32 device-to-device copy (torch copy_, "
                                         "read + write bytes), HIP events"},
         }
+        if pipe is not None:
+            line["pipelined"] = pipe
         if dry:
             line["dry_run"] = True
         if world == 1 and not args.no_cpu_baseline and not dry:
