@@ -977,7 +977,7 @@ struct WaveSolver {
     }
 #endif
     if (!wuni(w, ok)) return false;
-    wsync(w);  // records (P, p, K, k0, k1) visible to every lane
+    wsync(w);  // records (P, p, K, k) visible to every lane
     return true;
   }
 
@@ -1190,7 +1190,7 @@ struct WaveSolver {
       T Pn[NP], sw[6], rhs[6], wv[6];
       for (int i = 0; i < NP; ++i) Pn[i] = Rn[RCF::P + i];
       for (int i = 0; i < 6; ++i) {
-        T v = Rn[RCF::PV0 + i];  // p = p0 + mu p1 (riccati)
+        T v = Rn[RCF::PV0 + i];  // p (the Riccati's, mu already in)
         for (int l = 0; l < NX; ++l) v += Pn[pidx(i, l)] * dx[l];
         rhs[i] = v + cb[(CSF::CGW0 + i) * WL + k] + mu * cb[(CSF::CGW1 + i) * WL + k];
         sw[i] = cb[(CSF::CSW + i) * WL + k];
@@ -1202,7 +1202,7 @@ struct WaveSolver {
       // multiplier step dnu_{k+1} = P_{k+1} dx_{k+1} + p_{k+1} (correction form, eval_sweep)
       if (ln == k + 1)
         for (int i = 0; i < NX; ++i) {
-          T v = Rn[RCF::PV0 + i];  // p = p0 + mu p1 (riccati)
+          T v = Rn[RCF::PV0 + i];  // p (the Riccati's, mu already in)
           for (int l = 0; l < NX; ++l) v += Pn[pidx(i, l)] * dx[l];
           S(SSF::DNU + i) = v;  // correction form: the multiplier step itself
         }
