@@ -77,6 +77,8 @@ MR_HD float mr_rsqrt(float a) { return 1.0f / sqrtf(a); }
 
 template <typename T> MR_HD T mr_max(T a, T b) { return a > b ? a : b; }
 template <typename T> MR_HD T mr_min(T a, T b) { return a < b ? a : b; }
+// machine epsilon of the solve precision (IPOPT's Compare_le tolerance 10 eps |ref|)
+template <typename T> MR_HD constexpr T mr_eps() { return sizeof(T) == 8 ? T(2.220446049250313e-16) : T(1.1920928955078125e-07); }
 
 // models/VehicleParameters.py:3-41 (runtime values so a caller may change them,
 // as the reference's class attributes can be).

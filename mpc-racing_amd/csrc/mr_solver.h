@@ -23,6 +23,9 @@
 // monotone barrier update, fraction to the boundary, inertia correction, filter
 // line search) plus a second-order correction that re-rolls the shooting states.
 #pragma once
+#ifdef MR_RESTO_DEBUG
+#include <cstdio>
+#endif
 #include "mr_common.h"
 #include "gen_dynamics.h"
 #ifndef MR_PROF
@@ -67,16 +70,28 @@ struct WF {
     DS = DLAM + NI, DNU = DS + NI, H = DNU + NX, G0 = H + NH, G1 = G0 + NZ, GL = G1 + NZ,
     J = GL + NZ, C = J + 48, P = C + NX, PV0 = P + NP, PV1 = PV0 + NX, K = PV1 + NX, K0 = K + NU * NX,
     K1 = K0 + NU,
+    // IPOPT's inequality-row multipliers y_d (slot of the row: every box slot, the lower slot of a
+    // two-sided row) and their step; the slack block's share of the inertia correction (delta_s):
+    // HD = sum over rows of a a^T, GD = sum of a (d - s); the Cholesky factor of Q_uu (second-order
+    // corrections re-solve on the stored factorisation)
+    Y = K1 + NU, DY = Y + NI, HD = DY + NI, GD = HD + NH, LQ = GD + NZ,
+    // second-order correction: the accumulated right-hand sides c_soc (dynamics rows) / r_soc (rows),
+    // its direction and the vector part of its backward pass
+    SC = LQ + 6, SR = SC + NX, SDZ = SR + NI, SDS = SDZ + NZS, SDLAM = SDS + NI, SDY = SDLAM + NI,
+    SDNU = SDY + NI, SPV = SDNU + NX, SK0 = SPV + NX,
     // watchdog snapshot: the iterate and the search direction where the watchdog started
-    WZ = K1 + NU, WSL = WZ + NZS, WLAM = WSL + NI, WDZ = WLAM + NI, WDS = WDZ + NZS,
-    WDLAM = WDS + NI, WDNU = WDLAM + NI,
+    WZ = SK0 + NU, WSL = WZ + NZS, WLAM = WSL + NI, WDZ = WLAM + NI, WDS = WDZ + NZS,
+    WDLAM = WDS + NI, WDNU = WDLAM + NI, WY = WDNU + NX, WDY = WY + NI,
     // restoration phase: row relaxations p, n, their bound duals and steps, the reference point z_R
-    RP = WDNU + NX, RN = RP + NI, RVP = RN + NI, RVN = RVP + NI, RDP = RVN + NI, RDN = RDP + NI, RDVP = RDN + NI,
+    RP = WDY + NI, RN = RP + NI, RVP = RN + NI, RVN = RVP + NI, RDP = RVN + NI, RDN = RDP + NI, RDVP = RDN + NI,
     RDVN = RDVP + NI, RY = RDVN + NI, RDY = RY + NI, RZ = RDY + NI,
     // restoration relaxations of the 6 vehicle dynamics rows of x_{k+1} = F(x_k, u_k) (stage k < N):
     // p, n, duals, steps, and the condensed disturbance weight / gradient for the Riccati sweep
     CP = RZ + NZS, CN = CP + 6, CVP = CN + 6, CVN = CVP + 6, CDP = CVN + 6, CDN = CDP + 6, CDVP = CDN + 6,
-    CDVN = CDVP + 6, CSW = CDVN + 6, CGW0 = CSW + 6, CGW1 = CGW0 + 6, NF = CGW1 + 6
+    CDVN = CDVP + 6, CSW = CDVN + 6, CGW0 = CSW + 6, CGW1 = CGW0 + 6,
+    // the restoration phase's entry point (slacks, bound duals: the bound-multiplier update on return)
+    // and IPOPT's stored acceptable iterate (returned if the line search fails at an almost feasible point)
+    RS0 = CGW1 + 6, RLAM = RS0 + NI, AZ = RLAM + NI, NF = AZ + NZS
   };
 };
 
@@ -250,8 +265,27 @@ struct Row {
   int lane;
 };
 
+// IPOPT's bound_relax_factor (1e-8), capped by constr_viol_tol (1e-4): every inequality bound handed to
+// IPOPT is relaxed by min(1e-4, 1e-8 max(1, |b|)) before the solve (equality rows are not).
 template <typename T>
-MR_HD void make_row(const ProbParams<T>& P, const Inst<T>& I, int k, int r, const T* z, const Err<T>* e, Row<T>& R) {
+MR_HD T relax_amt(T b) { return mr_min(T(1e-4), T(1e-8) * mr_max(T(1), mr_abs(b))); }
+// Opti's rows as IPOPT receives them (oracle.nlp.MPCProblem.ipopt_ineq): the throttle / steer boxes are
+// two separate one-sided rows each (U < d_max, U > min: MPC.py:138-141), so the two slots of rows 0 / 1
+// are independent IPOPT rows (own slack, own multiplier y, linear damping kappa_d); every other row is an
+// opti.bounded row (MPC.py:134, :142-149, lane :135) -- ONE IPOPT slack s with two bounds, held here as
+// the pair of distances t_L = s - lo (slot 2r) and t_U = hi - s (slot 2r + 1, moved rigidly with t_L:
+// dt_U = -dt_L), its multiplier y in slot 2r.
+MR_HD constexpr bool two_sided_row(int r) { return r >= 2; }
+// slot j holds a row multiplier y (every slot of rows 0 / 1, the lower slot of a two-sided row)
+MR_HD constexpr bool yslot(int j) { return j < 4 || (j < JL + 2 && (j & 1) == 0); }
+// one-sided slots (the box rows): kappa_d damping
+MR_HD constexpr bool oneslot(int j) { return j < 4; }
+// sign of slot j's distance in IPOPT's slack: t = s - lo (lower, +1) or hi - s (upper, -1)
+MR_HD constexpr int slot_sign(int j) { return (j & 1) ? -1 : 1; }
+
+template <typename T>
+MR_HD void make_row_raw(const ProbParams<T>& P, const Inst<T>& I, int k, int r, const T* z, const Err<T>* e,
+                        Row<T>& R) {
   const int N = P.N;
   R.active = 0; R.n = 0; R.lane = 0; R.c = T(0); R.lo = T(0); R.hi = T(0);
   if (k == N) return;  // terminal stage: only the lane rows (lane_active)
@@ -289,16 +323,25 @@ MR_HD void make_row(const ProbParams<T>& P, const Inst<T>& I, int k, int r, cons
   }
 }
 
-// Lane rows on states i = 1..N (the commented MPC.py:135), two one-sided rows as the reference's
-// opti.bounded(-max_error, e_hat_C, max_error): e_C + m >= 0, m - e_C >= 0.  An infeasible start is the
-// restoration phase's business (IPOPT's way), not an elastic reformulation.
+template <typename T>
+MR_HD void make_row(const ProbParams<T>& P, const Inst<T>& I, int k, int r, const T* z, const Err<T>* e, Row<T>& R) {
+  make_row_raw(P, I, k, r, z, e, R);
+  R.lo -= relax_amt(R.lo);
+  R.hi += relax_amt(R.hi);
+}
+
+// Lane rows on states i = 1..N (the commented MPC.py:135): the reference's
+// opti.bounded(-max_error, e_hat_C, max_error), one IPOPT row with two (relaxed) bounds, held as the
+// distances e_C + m >= 0 (slot JL) and m - e_C >= 0 (JL + 1).  An infeasible start is the restoration
+// phase's business (IPOPT's way), not an elastic reformulation.
 template <typename T>
 MR_HD bool lane_active(const ProbParams<T>& P, int k) { return P.lane && k >= 1; }
 
 template <typename T>
 MR_HD void lane_d(const Inst<T>& I, T eC, T t, T* d) {  // t: the unused slot 14 (0)
-  d[0] = eC + I.max_err + t;
-  d[1] = I.max_err - eC + t;
+  const T m = I.max_err + relax_amt(I.max_err);
+  d[0] = eC + m + t;
+  d[1] = m - eC + t;
   d[2] = t;
 }
 
@@ -638,13 +681,20 @@ struct SolveOut {
 };
 
 #ifndef MR_FMAX
-#define MR_FMAX 16
+#define MR_FMAX 32  // filter entries kept (IPOPT: unbounded; the oracle's longest filter on the audits is 32)
 #endif
 #ifndef MR_FILTER_RESET_TRIGGER
 #define MR_FILTER_RESET_TRIGGER 5  // IPOPT filter_reset_trigger (0: heuristic off)
 #endif
 #ifndef MR_MAX_FILTER_RESETS
 #define MR_MAX_FILTER_RESETS 5  // IPOPT max_filter_resets
+#endif
+// IPOPT's tiny-step rule (tiny_step_tol 10 eps): off.  Its trigger is a step below 10 eps relative, i.e.
+// below the rounding noise of IPOPT's absolutely formed Lagrangian gradient at a converged point (the
+// oracle's dense restatement shows ~1e-14 relative steps there and never triggers it on the audited
+// instances); the correction-form residuals here are ~100x cleaner and would stop solves IPOPT continues.
+#ifndef MR_TINY_STEP
+#define MR_TINY_STEP 0
 #endif
 #ifndef MR_LS_FAIL_MAX
 #define MR_LS_FAIL_MAX 1000000
@@ -656,6 +706,23 @@ struct SolveOut {
 #define MR_WD_TRIAL_MAX 3  // IPOPT watchdog_trial_iter_max
 #endif
 constexpr int FMAX = MR_FMAX;
+
+// IPOPT 3.14 option defaults the solver restates beyond W&B 2006's line-search constants (the dense
+// restatement oracle/ipopt.py implements the same rules; DESIGN.md §2 lists them)
+constexpr double IP_KAPPA_D = 1e-5;                                                     // kappa_d
+constexpr double IP_CONSTR_VIOL_TOL = 1e-4, IP_COMPL_INF_TOL = 1e-4, IP_DUAL_INF_TOL = 1.0;  // unscaled
+constexpr double IP_ACC_DUAL_INF = 1e10, IP_ACC_CONSTR_VIOL = 1e-2, IP_ACC_COMPL = 1e-2;      // acceptable_*
+constexpr double IP_OBJ_MAX_INC = 5.0, IP_KAPPA_SOC = 0.99, IP_MULT_INIT_MAX = 1000.0;
+constexpr int IP_MAX_SOC = 4;
+// backtracking halvings per line search (IPOPT has no cap; a_min > 0 ends it unless theta is exactly 0)
+constexpr int IP_LS_MAX = 200;
+
+// Reference values of a line search (FilterLSAcceptor's reference point: the current iterate, or the
+// watchdog's stored point)
+template <typename T>
+struct LSRef {
+  T th, ph, gphi, thpow;
+};
 
 template <typename T, int MODEL>
 struct Solver {
@@ -670,9 +737,14 @@ struct Solver {
   T theta_max, theta_min;
   T filt_th[FMAX], filt_ph[FMAX];
   int nfilt;
-  // iteration aggregates (eval sweep)
-  T stat_max, pr_max, theta, slam_max, slam_min, nu1, lam1, fval, logs;
-  int me, mi;
+  // iteration aggregates (eval sweep): dual infeasibility (stat), primal infeasibility of the equality
+  // rows (pr_eq) and of the inequality rows' d - s (pr_rows; pr_max = both), the violation of the
+  // inequality rows' bounds (viol), theta, complementarity extremes, multiplier 1-norms, f, barrier sums
+  T stat_max, pr_max, pr_eq, viol_max, theta, slam_max, slam_min, nu1, y1, lam1, fval, logs, lins;
+  T pr_o;  // restoration phase: the original problem's primal infeasibility at the current point
+  int me, mi, mrow;
+  T delta_it;  // the accepted factorisation's delta (slack block: delta_s = delta_x)
+  bool rej_filter = false;
   // restoration phase: mode, its penalty and proximity weight, and the original problem's state
   bool resto = false;
   T rho = T(RESTO_RHO), zeta = T(0);
@@ -680,6 +752,7 @@ struct Solver {
   T ofilt_th[FMAX], ofilt_ph[FMAX];
   int onfilt;
   T tho_acc, pho_acc;  // original theta / barrier objective of the last trial point (restoration)
+  bool have_acc = false;  // an acceptable iterate is stored (AZ)
   double* trace = nullptr;  // optional per-iteration record (diagnostics)
   int trace_cap = 0;
   // the dynamics rows' multipliers nu_k (x_k = F(x_{k-1}, u_{k-1}), k >= 1) and their watchdog copy, fp64
@@ -714,8 +787,21 @@ struct Solver {
     act[JL + 2] = 0;  // (slot JL + 2 unused)
     lane_d(I, e.eC, z[14], d + JL);
   }
+  // the row gradient a (stage indices, values) of slot pair r (< NROW) or the lane rows (r == NROW)
+  MR_HD int row_grad(int r, const Row<T>* rows, const Err<T>& e, int* idx, T* a) const {
+    if (r < NROW) {
+      for (int q = 0; q < rows[r].n; ++q) { idx[q] = rows[r].idx[q]; a[q] = rows[r].a[q]; }
+      return rows[r].n;
+    }
+    idx[0] = 0; idx[1] = 1; idx[2] = 6;
+    a[0] = e.gC[0]; a[1] = e.gC[1]; a[2] = e.gC[2];
+    return 3;
+  }
+  // IPOPT's residual c - s of the row in slot j (a y-slot) from the slot distances: box lower d - t,
+  // box upper -(d - t), two-sided d_L - t_L
+  static MR_HD T ipopt_res(int j, const T* d, const T* t) { return T(slot_sign(j)) * (d[j] - t[j]); }
 
-  // ---------------- initialisation (MPC.py:100-131) ----------------
+  // ---------------- initialisation (MPC.py:100-131; IPOPT's DefaultIterateInitializer) ----------------
   // u_init: optional strided [2][N] initial controls of this instance (element (r, k) at u_init[(r*N+k)*ustride])
   MR_HD void init(const double* u_init, int64_t ustride) {
     cur = 0;
@@ -737,10 +823,6 @@ struct Solver {
       errors(I, z[0], z[1], z[6], e, false);
       z[14] = T(0);
       store_z(k, 0, z);
-#ifdef MR_DEBUG_PRINT
-      if (trace) printf("init k=%d vx=%g readback=%g X=%g S=%g\n", k, (double)z[3], (double)W(k, WF::Z0 + 3),
-                        (double)z[0], (double)z[6]);
-#endif
       // objective gradient for the gradient-based scaling
       T g[NZ];
       for (int i = 0; i < NZ; ++i) g[i] = T(0);
@@ -752,7 +834,9 @@ struct Solver {
       }
     }
     sc = gmax > T(0) ? mr_min(T(1), T(100) / gmax) : T(1);
-    // slacks (IPOPT bound push), multipliers
+    // slacks (IPOPT's slack_bound_push / slack_bound_frac 1e-2: a one-sided row's slack at least
+    // 1e-2 max(1, |b|) inside its bound; a two-sided row's slack s projected into [lo + p_L, hi - p_U],
+    // p = min(1e-2 max(1, |b|), 1e-2 (hi - lo))), bound duals 1, multipliers 0 (ls_init below)
     T th = T(0);
     for (int k = 0; k <= N; ++k) {
       load_z(k, 0, z);
@@ -762,20 +846,33 @@ struct Solver {
       int act[NI];
       Row<T> rows[NROW];
       row_values(k, z, e, d, act, rows);
-      for (int j = 0; j < NI; ++j) {
-        T push;
-        if (j < JL) {
-          const Row<T>& R = rows[j / 2];
-          T bnd = (j & 1) ? mr_abs(R.hi) : mr_abs(R.lo);
-          push = mr_min(T(1e-2) * mr_max(T(1), bnd), T(1e-2) * (R.hi - R.lo));
+      T t[NI];
+      for (int j = 0; j < NI; ++j) t[j] = T(1);
+      for (int r = 0; r <= NROW; ++r) {
+        const int j0 = r < NROW ? 2 * r : JL;
+        if (!act[j0]) continue;
+        if (r < 2) {  // the box rows: two one-sided rows
+          t[j0] = mr_max(d[j0], T(1e-2) * mr_max(T(1), mr_abs(rows[r].lo)));
+          t[j0 + 1] = mr_max(d[j0 + 1], T(1e-2) * mr_max(T(1), mr_abs(rows[r].hi)));
         } else {
-          push = j < JL + 2 ? T(1e-2) * mr_max(T(1), I.max_err) : T(1e-2);
+          T c, lo, hi;
+          if (r < NROW) { c = rows[r].c; lo = rows[r].lo; hi = rows[r].hi; }
+          else { hi = I.max_err + relax_amt(I.max_err); lo = -hi; c = e.eC; }
+          const T rng = hi - lo;
+          const T pL = mr_min(T(1e-2) * mr_max(T(1), mr_abs(lo)), T(1e-2) * rng);
+          const T pU = mr_min(T(1e-2) * mr_max(T(1), mr_abs(hi)), T(1e-2) * rng);
+          const T sv = mr_min(mr_max(c, lo + pL), hi - pU);
+          t[j0] = sv - lo;
+          t[j0 + 1] = hi - sv;
         }
-        T s = act[j] ? mr_max(d[j], push) : T(1);
-        W(k, WF::S0 + j) = s;
+      }
+      for (int j = 0; j < NI; ++j) {
+        W(k, WF::S0 + j) = t[j];
         W(k, WF::LAM + j) = act[j] ? T(1) : T(0);
         W(k, WF::DLAM + j) = T(0);
-        if (act[j]) th += mr_abs(d[j] - s);
+        W(k, WF::Y + j) = T(0);
+        W(k, WF::DY + j) = T(0);
+        if (act[j] && yslot(j)) th += mr_abs(d[j] - t[j]);
       }
       for (int i = 0; i < NX; ++i) { nub[k][i] = 0.0; W(k, WF::DNU + i) = T(0); }
     }
@@ -785,6 +882,119 @@ struct Solver {
     theta_max = T(1e4) * mr_max(T(1), th);
     theta_min = T(1e-4) * mr_max(T(1), th);
     nfilt = 0;
+    have_acc = false;
+    ls_init();
+  }
+
+  // IPOPT's least-square multipliers (constr_mult_init_max 1000): y_c, y_d minimising
+  // ||grad_x L||^2 + ||grad_s L||^2 at the initial point, i.e. the augmented system with W = 0,
+  // D_x = D_s = I -- here the stage QP  min 1/2 sx' M sx + g' sx  s.t. the linearised dynamics with
+  // c = 0, M = I on the reference's variables (delta_var) + sum over rows a a^T, g = grad f - sum a rs
+  // (rs = v_L - v_U of the row), solved by the Riccati recursion: the costates are the dynamics rows'
+  // multipliers, y_d = a.sx - rs.  Both are set to zero if one exceeds 1000 in magnitude.
+  MR_HD void ls_init() {
+    T z[NZS];
+    for (int k = 0; k <= N; ++k) {
+      load_z(k, 0, z);
+      T H[NH], g[NZ], J[48];
+      for (int i = 0; i < NH; ++i) H[i] = T(0);
+      for (int i = 0; i < NZ; ++i) g[i] = T(0);
+      for (int i = 0; i < 48; ++i) J[i] = T(0);
+      if (k < N) {
+        T Hd[36], fx[6], nz[NX];
+        for (int i = 0; i < NX; ++i) nz[i] = T(0);
+        Dyn<T, MODEL>::fjh(P, z, z + NX, nz, fx, J, Hd);
+      }
+      for (int i = 0; i < NZ; ++i)
+        if (delta_var(i)) H[hidx(i, i)] = T(1);
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      stage_cost(P, I, k, z, e, sc, g, (T*)nullptr);
+      T d[NI];
+      int act[NI];
+      Row<T> rows[NROW];
+      row_values(k, z, e, d, act, rows);
+      for (int r = 0; r <= NROW; ++r) {
+        const int j0 = r < NROW ? 2 * r : JL;
+        if (!act[j0]) continue;
+        int idx[3];
+        T a[3];
+        const int na = row_grad(r, rows, e, idx, a);
+        // the IPOPT rows on this gradient: two one-sided (box) or one two-sided, each a a^T; rs = v_L - v_U
+        const T nrow = r < 2 ? T(2) : T(1);
+        const T rs = r < 2 ? (W(k, WF::LAM + j0) - W(k, WF::LAM + j0 + 1)) : T(0);
+        for (int q = 0; q < na; ++q) {
+          g[idx[q]] -= a[q] * rs;
+          for (int q2 = q; q2 < na; ++q2) H[hidx(idx[q], idx[q2])] += nrow * a[q] * a[q2];
+        }
+      }
+      for (int i = 0; i < NH; ++i) { W(k, WF::H + i) = H[i]; W(k, WF::HD + i) = T(0); }
+      for (int i = 0; i < NZ; ++i) { W(k, WF::G0 + i) = g[i]; W(k, WF::G1 + i) = T(0); W(k, WF::GD + i) = T(0); }
+      for (int i = 0; i < NX; ++i) W(k, WF::C + i) = T(0);
+      for (int i = 0; i < 48; ++i) W(k, WF::J + i) = J[i];
+    }
+    if (!riccati(T(0))) return;  // (M is positive definite on the dynamics' null space; never fails)
+    // forward: sx and the costates
+    T dx[NX];
+    for (int i = 0; i < NX; ++i) dx[i] = T(0);
+    bool ok = true;
+    const T big = T(IP_MULT_INIT_MAX);
+    for (int k = 0; k <= N; ++k) {
+      T dz[NZS];
+      for (int i = 0; i < NZS; ++i) dz[i] = T(0);
+      for (int i = 0; i < NX; ++i) dz[i] = dx[i];
+      if (k < N)
+        for (int a = 0; a < NU; ++a) {
+          T v = W(k, WF::K0 + a);
+          for (int j = 0; j < NX; ++j) v += W(k, WF::K + a * NX + j) * dx[j];
+          dz[NX + a] = v;
+        }
+      // costate of stage k: the multipliers of x_k = F(x_{k-1}, u_{k-1}) (k >= 1) or of the
+      // initial-state rows (k = 0)
+      for (int i = 0; i < NX; ++i) {
+        T v = W(k, WF::PV0 + i);
+        for (int l = 0; l < NX; ++l) v += W(k, WF::P + pidx(i, l)) * dx[l];
+        nub[k][i] = (double)v;
+        if (i < 6 || (k == 0 && i == 6)) ok = ok && (mr_abs(v) <= big);
+      }
+      load_z(k, 0, z);
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      T d[NI];
+      int act[NI];
+      Row<T> rows[NROW];
+      row_values(k, z, e, d, act, rows);
+      for (int r = 0; r <= NROW; ++r) {
+        const int j0 = r < NROW ? 2 * r : JL;
+        if (!act[j0]) continue;
+        int idx[3];
+        T a[3];
+        const int na = row_grad(r, rows, e, idx, a);
+        T adz = T(0);
+        for (int q = 0; q < na; ++q) adz += a[q] * dz[idx[q]];
+        if (r < 2) {  // y_d = a.sx - rs per one-sided row: rs = v_L (lower) / -v_U (upper)
+          const T y0 = adz - W(k, WF::LAM + j0), y1 = adz + W(k, WF::LAM + j0 + 1);
+          W(k, WF::Y + j0) = y0;
+          W(k, WF::Y + j0 + 1) = y1;
+          ok = ok && mr_abs(y0) <= big && mr_abs(y1) <= big;
+        } else {
+          W(k, WF::Y + j0) = adz;
+          ok = ok && mr_abs(adz) <= big;
+        }
+      }
+      if (k < N) {
+        T J[48], t[NX], tb[NX];
+        for (int i = 0; i < 48; ++i) J[i] = W(k, WF::J + i);
+        apply_A(J, k, dx, t);
+        apply_B(J, k, dz + NX, tb);
+        for (int i = 0; i < NX; ++i) dx[i] = t[i] + tb[i];
+      }
+    }
+    if (!(ok == ok) || !ok)
+      for (int k = 0; k <= N; ++k) {
+        for (int i = 0; i < NX; ++i) nub[k][i] = 0.0;
+        for (int j = 0; j < NI; ++j) W(k, WF::Y + j) = T(0);
+      }
   }
 
   // ---------------- sweep 1: evaluation, KKT error, stage QP data ----------------
@@ -792,13 +1002,16 @@ struct Solver {
   MR_HD void eval_sweep(T mu_prev) {
     const T kappa_sigma = T(1e10);
     zeta = mr_sqrt(mu_prev);  // restoration proximity weight (IPOPT: resto_proximity_weight sqrt(mu))
-    stat_max = pr_max = theta = T(0);
+    stat_max = pr_eq = pr_max = viol_max = theta = T(0);
+    pr_o = T(0);
     slam_max = T(0);
     slam_min = T(1e30);
-    nu1 = lam1 = fval = logs = T(0);
+    nu1 = y1 = lam1 = fval = logs = lins = T(0);
+    T pr_rows = T(0);
     const bool refk = !MR_KKT_RESTATED && !resto;  // the optimality error on the reference's NLP
     me = refk ? 6 * N + 7 : NX * (N + 1);
     mi = 0;
+    mrow = 0;
     if (refk)  // multipliers of the initial-state rows X_0 = state0, S_0 = s0 (lazy update, as nu_{k >= 1})
       for (int i = 0; i <= 6; ++i) {
         nub[0][i] += (double)alpha_p * (double)W(0, WF::DNU + i);
@@ -818,16 +1031,11 @@ struct Solver {
           if (!refk || i < 6) nu1 += mr_abs(nun[i]);
         }
         load_z(k + 1, cur, znext);
-#ifdef MR_DEBUG_PRINT
-        if (trace && mu_prev == T(0.1) && alpha_p == T(0))
-          printf("eval k=%d cur=%d z.vx=%g znext.vx=%g znext.X=%g\n", k, cur, (double)z[3], (double)znext[3],
-                 (double)znext[0]);
-#endif
       }
-      T H[NH], g0[NZ], g1[NZ], gl[NZ], st[NZ];
+      T H[NH], g0[NZ], g1[NZ], gl[NZ], st[NZ], HD[NH], GD[NZ];
       double dd[NZ];
-      for (int i = 0; i < NH; ++i) H[i] = T(0);
-      for (int i = 0; i < NZ; ++i) { g0[i] = g1[i] = gl[i] = st[i] = T(0); dd[i] = 0.0; }
+      for (int i = 0; i < NH; ++i) { H[i] = T(0); HD[i] = T(0); }
+      for (int i = 0; i < NZ; ++i) { g0[i] = g1[i] = gl[i] = st[i] = GD[i] = T(0); dd[i] = 0.0; }
       if (k < N) {
         T Hd[36], J[48], fx[6];
         Dyn<T, MODEL>::fjh(P, z, z + NX, nun, fx, J, Hd);
@@ -844,8 +1052,8 @@ struct Solver {
         c[8] = z[12] - znext[8];
         c[9] = (k == 0 ? z[11] : z[9]) - znext[9];
         c[10] = (k == 0 ? z[12] : z[10]) - znext[10];
+        for (int i = 0; i < NX; ++i) pr_o = mr_max(pr_o, mr_abs(c[i]));
         if (resto) {  // relaxed vehicle rows F - x' - p + n (the S / previous-control rows are definitions)
-          const T kappa_sigma = T(1e10);
           for (int i = 0; i < 6; ++i) {
             const T p = W(k, WF::CP + i), n = W(k, WF::CN + i);
             T vp = W(k, WF::CVP + i) + alpha_d * W(k, WF::CDVP + i);
@@ -871,7 +1079,7 @@ struct Solver {
         }
         for (int i = 0; i < NX; ++i) {
           W(k, WF::C + i) = c[i];
-          pr_max = mr_max(pr_max, mr_abs(c[i]));
+          pr_eq = mr_max(pr_eq, mr_abs(c[i]));
           theta += mr_abs(c[i]);
         }
         for (int i = 0; i < 48; ++i) W(k, WF::J + i) = J[i];
@@ -902,16 +1110,18 @@ struct Solver {
       int act[NI];
       Row<T> rows[NROW];
       row_values(k, z, e, d, act, rows);
-      T lam_j[NI], sig_j[NI], c0_j[NI], c1_j[NI], y_j[NI];  // y: the row multiplier in W and grad L
+      T lam_j[NI], sig_j[NI], c0_j[NI], c1_j[NI], y_j[NI], t_j[NI];
       auto clip = [&](T v, T x) { return mr_min(mr_max(v, mu_prev / (kappa_sigma * x)), kappa_sigma * mu_prev / x); };
       for (int j = 0; j < NI; ++j) {
         lam_j[j] = sig_j[j] = c0_j[j] = c1_j[j] = y_j[j] = T(0);
+        t_j[j] = T(1);
         if (!act[j]) continue;
         T s = W(k, sf(cur) + j);
         T lam = clip(W(k, WF::LAM + j) + alpha_d * W(k, WF::DLAM + j), s);
         W(k, WF::LAM + j) = lam;
         lam_j[j] = lam;
-        y_j[j] = lam;  // regular phase: the slack's bound dual is the row multiplier
+        t_j[j] = s;
+        sig_j[j] = lam / s;
         T rd = d[j] - s;
         T sl = s * lam;
         slam_max = mr_max(slam_max, sl);
@@ -919,6 +1129,7 @@ struct Solver {
         lam1 += mr_abs(lam);
         logs += mr_log(s);
         mi += 1;
+        viol_max = mr_max(viol_max, -d[j]);  // bound violation of the row value (max with 0: viol_max >= 0)
         if (resto) {
           const T p = W(k, WF::RP + j), n = W(k, WF::RN + j);
           const T vp = clip(W(k, WF::RVP + j) + alpha_d * W(k, WF::RDVP + j), p);
@@ -930,10 +1141,8 @@ struct Solver {
           const T y = W(k, WF::RY + j) + alpha_p * W(k, WF::RDY + j);
           W(k, WF::RY + j) = y;
           y_j[j] = y;
-#ifndef MR_RESTO_YSTAT
-#define MR_RESTO_YSTAT 1
-#endif
-          if (MR_RESTO_YSTAT) stat_max = mr_max(stat_max, mr_abs(y - lam));
+          stat_max = mr_max(stat_max, mr_abs(y - lam));
+          if (yslot(j)) pr_o = mr_max(pr_o, mr_abs(rd));
           rd = rd - p + n;
           slam_max = mr_max(slam_max, mr_max(p * vp, n * vn));
           slam_min = mr_min(slam_min, mr_min(p * vp, n * vn));
@@ -943,44 +1152,99 @@ struct Solver {
           fval += rho * (p + n);
           stat_max = mr_max(stat_max, mr_max(mr_abs(rho + y - vp), mr_abs(rho - y - vn)));
           row_cond_r(d[j], s, lam, p, n, vp, vn, rho, sig_j[j], c0_j[j], c1_j[j]);
-        } else {
-          row_cond(d[j], s, lam, sig_j[j], c0_j[j], c1_j[j]);
+          pr_rows = mr_max(pr_rows, mr_abs(rd));
+          theta += mr_abs(rd);
+        } else if (yslot(j)) {  // an IPOPT row: its multiplier y_d (lazy update with the primal step)
+          const T y = W(k, WF::Y + j) + alpha_p * W(k, WF::DY + j);
+          W(k, WF::Y + j) = y;
+          y_j[j] = y;
+          y1 += mr_abs(y);
+          mrow += 1;
+          pr_rows = mr_max(pr_rows, mr_abs(rd));
+          theta += mr_abs(rd);
         }
-        pr_max = mr_max(pr_max, mr_abs(rd));
-        theta += mr_abs(rd);
+        if (oneslot(j)) lins += s;
       }
-      for (int r = 0; r < NROW; ++r) {
-        const Row<T>& R = rows[r];
-        if (!R.active) continue;
-        T sig_sum = T(0), gsc0 = T(0), gsc1 = T(0), lamdiff = T(0);
-        for (int sd = 0; sd < 2; ++sd) {
-          int j = 2 * r + sd;
-          T sgn = sd == 0 ? T(1) : T(-1);
-          sig_sum += sig_j[j];
-          gsc0 += sgn * c0_j[j];
-          gsc1 += sgn * c1_j[j];
-          lamdiff += sgn * y_j[j];
+      if (resto) {
+        for (int r = 0; r < NROW; ++r) {
+          const Row<T>& R = rows[r];
+          if (!R.active) continue;
+          T sig_sum = T(0), gsc0 = T(0), gsc1 = T(0), lamdiff = T(0);
+          for (int sd = 0; sd < 2; ++sd) {
+            int j = 2 * r + sd;
+            T sgn = sd == 0 ? T(1) : T(-1);
+            sig_sum += sig_j[j];
+            gsc0 += sgn * c0_j[j];
+            gsc1 += sgn * c1_j[j];
+            lamdiff += sgn * y_j[j];
+          }
+          for (int a = 0; a < R.n; ++a) {
+            g0[R.idx[a]] += R.a[a] * gsc0;
+            g1[R.idx[a]] += R.a[a] * gsc1;
+            st[R.idx[a]] -= lamdiff * R.a[a];
+            for (int bb = a; bb < R.n; ++bb) H[hidx(R.idx[a], R.idx[bb])] += sig_sum * R.a[a] * R.a[bb];
+          }
         }
-        for (int a = 0; a < R.n; ++a) {
-          g0[R.idx[a]] += R.a[a] * gsc0;
-          g1[R.idx[a]] += R.a[a] * gsc1;
-          st[R.idx[a]] -= lamdiff * R.a[a];
-          for (int bb = a; bb < R.n; ++bb) H[hidx(R.idx[a], R.idx[bb])] += sig_sum * R.a[a] * R.a[bb];
+        if (lane_active(P, k)) {
+          const int id3[3] = {0, 1, 6};
+          const T sig_sum = sig_j[JL] + sig_j[JL + 1];
+          const T gz0 = c0_j[JL] - c0_j[JL + 1], gz1 = c1_j[JL] - c1_j[JL + 1];
+          const T lamdiff = y_j[JL] - y_j[JL + 1];
+          int q = 0;
+          for (int a = 0; a < 3; ++a) {
+            g0[id3[a]] += e.gC[a] * gz0;
+            g1[id3[a]] += e.gC[a] * gz1;
+            st[id3[a]] -= lamdiff * e.gC[a];
+            for (int bb = a; bb < 3; ++bb, ++q)
+              H[hidx(id3[a], id3[bb])] += sig_sum * e.gC[a] * e.gC[bb] - lamdiff * e.hC[q];
+          }
         }
-      }
-      if (lane_active(P, k)) {
-        // hard lane rows e_C + m >= 0 (slot JL) and m - e_C >= 0 (JL+1), nonlinear in (X, Y, S)
-        const int id3[3] = {0, 1, 6};
-        const T sig_sum = sig_j[JL] + sig_j[JL + 1];
-        const T gz0 = c0_j[JL] - c0_j[JL + 1], gz1 = c1_j[JL] - c1_j[JL + 1];
-        const T lamdiff = y_j[JL] - y_j[JL + 1];
-        int q = 0;
-        for (int a = 0; a < 3; ++a) {
-          g0[id3[a]] += e.gC[a] * gz0;
-          g1[id3[a]] += e.gC[a] * gz1;
-          st[id3[a]] -= lamdiff * e.gC[a];
-          for (int bb = a; bb < 3; ++bb, ++q)
-            H[hidx(id3[a], id3[bb])] += sig_sum * e.gC[a] * e.gC[bb] - lamdiff * e.hC[q];
+      } else {
+        // IPOPT's rows condensed into the stage QP (slacks eliminated):  H += (Sigma_s) a a^T,
+        // g += a (Sigma_s (d - s) + grad_s phi) with grad_s phi = -mu/t_L + mu/t_U (+-kappa_d mu for a
+        // one-sided row) split into its mu-free (g0) and mu (g1) parts; the Lagrangian gradient gets
+        // y a (L = f + y (d - s)), the slack's stationarity -y - v_L + v_U enters the dual infeasibility;
+        // HD / GD: the inertia correction's slack shift delta_s = delta (delta a a^T, delta a (d - s))
+        for (int r = 0; r <= NROW; ++r) {
+          const int j0 = r < NROW ? 2 * r : JL, j1 = j0 + 1;
+          if (!act[j0]) continue;
+          int idx[3];
+          T a[3];
+          const int na = row_grad(r, rows, e, idx, a);
+          T hs, gr0, gr1, ys, hdw, gdw;
+          if (r < 2) {  // two one-sided rows: lower (c >= lo) in j0, upper (c <= hi) in j1
+            hs = sig_j[j0] + sig_j[j1];
+            gr0 = sig_j[j0] * (d[j0] - t_j[j0]) - sig_j[j1] * (d[j1] - t_j[j1]);
+            gr1 = (-T(1) / t_j[j0] + T(IP_KAPPA_D)) + (T(1) / t_j[j1] - T(IP_KAPPA_D));
+            ys = y_j[j0] + y_j[j1];
+            hdw = T(2);
+            gdw = (d[j0] - t_j[j0]) - (d[j1] - t_j[j1]);
+            stat_max = mr_max(stat_max, mr_max(mr_abs(-y_j[j0] - lam_j[j0]), mr_abs(-y_j[j1] + lam_j[j1])));
+          } else {  // one two-sided row: s = lo + t_L = hi - t_U
+            hs = sig_j[j0] + sig_j[j1];
+            gr0 = hs * (d[j0] - t_j[j0]);
+            gr1 = -T(1) / t_j[j0] + T(1) / t_j[j1];
+            ys = y_j[j0];
+            hdw = T(1);
+            gdw = d[j0] - t_j[j0];
+            stat_max = mr_max(stat_max, mr_abs(-y_j[j0] - lam_j[j0] + lam_j[j1]));
+          }
+          for (int q = 0; q < na; ++q) {
+            g0[idx[q]] += a[q] * gr0;
+            g1[idx[q]] += a[q] * gr1;
+            st[idx[q]] += ys * a[q];
+            GD[idx[q]] += a[q] * gdw;
+            for (int q2 = q; q2 < na; ++q2) {
+              H[hidx(idx[q], idx[q2])] += hs * a[q] * a[q2];
+              HD[hidx(idx[q], idx[q2])] += hdw * a[q] * a[q2];
+            }
+          }
+          if (r == NROW) {  // the lane row's curvature y * grad^2 e_C in (X, Y, S)
+            const int id3[3] = {0, 1, 6};
+            int q = 0;
+            for (int a3 = 0; a3 < 3; ++a3)
+              for (int b3 = a3; b3 < 3; ++b3, ++q) H[hidx(id3[a3], id3[b3])] += ys * e.hC[q];
+          }
         }
       }
       // stationarity: x-part for k >= 1, u-part for k < N
@@ -1007,35 +1271,64 @@ struct Solver {
           if (i < NX ? k >= 1 : k < N) stat_max = mr_max(stat_max, mr_abs(sti));
         }
       }
-      for (int i = 0; i < NH; ++i) W(k, WF::H + i) = H[i];
+      for (int i = 0; i < NH; ++i) { W(k, WF::H + i) = H[i]; W(k, WF::HD + i) = HD[i]; }
       for (int i = 0; i < NZ; ++i) {
         W(k, WF::G0 + i) = T((double)g0[i] + dd[i]);
         W(k, WF::G1 + i) = g1[i];
         W(k, WF::GL + i) = gl[i];
+        W(k, WF::GD + i) = GD[i];
       }
       // advance
       if (k < N)
         for (int i = 0; i < NZS; ++i) z[i] = znext[i];
     }
+    pr_max = mr_max(pr_eq, pr_rows);
   }
 
-  MR_HD T kkt_error(T m) const {
-    const T smax = T(100);
-    T sd = mr_max(smax, (nu1 + lam1) / T(me + (mi > 0 ? mi : 1))) / smax;
-    T scm = mr_max(smax, lam1 / T(mi > 0 ? mi : 1)) / smax;
-    T cerr = mr_max(mr_abs(slam_max - m), mr_abs(m - slam_min));
-    if (mi == 0) cerr = T(0);
-    return mr_max(mr_max(stat_max / sd, pr_max), cerr / scm);
+  // IPOPT's optimality-error scaling s_d (over y_c, y_d and the bound duals) and s_c
+  MR_HD T s_d() const {
+    return mr_max(T(100), (nu1 + y1 + lam1) / T(me + mrow + (mi > 0 ? mi : 1))) / T(100);
+  }
+  MR_HD T s_c() const { return mr_max(T(100), lam1 / T(mi > 0 ? mi : 1)) / T(100); }
+  MR_HD T compl_err(T m) const {
+    if (mi == 0) return T(0);
+    return mr_max(mr_abs(slam_max - m), mr_abs(m - slam_min));
+  }
+  // curr_nlp_error: the primal part is the violation of the constraints (|c| and d(x) outside its bounds)
+  MR_HD T nlp_error() const {
+    const T pr = resto ? pr_max : mr_max(pr_eq, viol_max);
+    return mr_max(mr_max(stat_max / s_d(), pr), compl_err(T(0)) / s_c());
+  }
+  // curr_barrier_error: the primal part is the infeasibility |c|, |d - s|
+  MR_HD T barrier_error(T m) const { return mr_max(mr_max(stat_max / s_d(), pr_max), compl_err(m) / s_c()); }
+  MR_HD T kkt_error(T m) const { return barrier_error(m); }
+  // IPOPT's unscaled termination quantities: dual infeasibility, constraint violation, complementarity
+  MR_HD bool converged(T err) const {
+    if (!(err <= P.tol)) return false;
+    return stat_max / sc <= T(IP_DUAL_INF_TOL) && mr_max(pr_eq, viol_max) <= T(IP_CONSTR_VIOL_TOL) &&
+           compl_err(T(0)) / sc <= T(IP_COMPL_INF_TOL);
+  }
+  MR_HD bool acceptable(T err) const {
+    if (!(err <= P.acc_tol)) return false;
+    return stat_max / sc <= T(IP_ACC_DUAL_INF) && mr_max(pr_eq, viol_max) <= T(IP_ACC_CONSTR_VIOL) &&
+           compl_err(T(0)) / sc <= T(IP_ACC_COMPL);
   }
 
   // ---------------- sweep 2: Riccati factorisation (backward) ----------------
+  // Stage QP data H + delta (I_var + HD), g + delta GD: IPOPT's inertia correction shifts the reference's
+  // variables (delta_x, delta_var) and the slacks (delta_s = delta_x; condensed: delta a a^T and
+  // delta a (d - s) per row, HD / GD from the evaluation sweep).
   MR_HD bool riccati(T delta) {
     T Pm[NP], p0[NX], p1[NX];
+    auto Hq = [&](int k, int i, int j) {
+      return W(k, WF::H + hidx(i, j)) + delta * W(k, WF::HD + hidx(i, j)) + (i == j && delta_var(i) ? delta : T(0));
+    };
+    auto Gq = [&](int k, int i) { return W(k, WF::G0 + i) + delta * W(k, WF::GD + i); };
     {
       const int k = N;
       for (int i = 0; i < NX; ++i)
-        for (int j = i; j < NX; ++j) Pm[pidx(i, j)] = W(k, WF::H + hidx(i, j)) + (i == j && delta_var(i) ? delta : T(0));
-      for (int i = 0; i < NX; ++i) { p0[i] = W(k, WF::G0 + i); p1[i] = W(k, WF::G1 + i); }
+        for (int j = i; j < NX; ++j) Pm[pidx(i, j)] = Hq(k, i, j);
+      for (int i = 0; i < NX; ++i) { p0[i] = Gq(k, i); p1[i] = W(k, WF::G1 + i); }
       for (int i = 0; i < NP; ++i) W(k, WF::P + i) = Pm[i];
       for (int i = 0; i < NX; ++i) { W(k, WF::PV0 + i) = p0[i]; W(k, WF::PV1 + i) = p1[i]; }
     }
@@ -1081,7 +1374,7 @@ struct Solver {
             for (int i = 0; i < NX; ++i) colb[i] = PB[i][b];
             T bt[NU];
             apply_Bt(J, k, colb, bt);
-            Rh[q] = W(k, WF::H + hidx(NX + a, NX + b)) + bt[a] + (a == b && delta_var(NX + a) ? delta : T(0));
+            Rh[q] = Hq(k, NX + a, NX + b) + bt[a];
           }
       }
       T Sh[NU][NX];
@@ -1089,10 +1382,11 @@ struct Solver {
         T colj[NX], bt[NU];
         for (int i = 0; i < NX; ++i) colj[i] = PA[i][j];
         apply_Bt(J, k, colj, bt);
-        for (int a = 0; a < NU; ++a) Sh[a][j] = W(k, WF::H + hidx(j, NX + a)) + bt[a];
+        for (int a = 0; a < NU; ++a) Sh[a][j] = Hq(k, j, NX + a) + bt[a];
       }
       T L[6];
       if (!chol3(Rh, L)) return false;
+      for (int q = 0; q < 6; ++q) W(k, WF::LQ + q) = L[q];
       // vector parts
       T pc0[NX];
       for (int i = 0; i < NX; ++i) {
@@ -1104,7 +1398,7 @@ struct Solver {
       apply_Bt(J, k, pc0, rh0);
       apply_Bt(J, k, p1, rh1);
       for (int a = 0; a < NU; ++a) {
-        rh0[a] += W(k, WF::G0 + NX + a);
+        rh0[a] += Gq(k, NX + a);
         rh1[a] += W(k, WF::G1 + NX + a);
       }
       T k0[NU] = {-rh0[0], -rh0[1], -rh0[2]}, k1[NU] = {-rh1[0], -rh1[1], -rh1[2]};
@@ -1123,7 +1417,7 @@ struct Solver {
         for (int i = 0; i < NX; ++i) colj[i] = PA[i][j];
         apply_At(J, k, colj, at);  // column j of A^T P A
         for (int i = 0; i <= j; ++i) {
-          T v = at[i] + W(k, WF::H + hidx(i, j)) + (i == j && delta_var(i) ? delta : T(0));
+          T v = at[i] + Hq(k, i, j);
           for (int a = 0; a < NU; ++a) v += Sh[a][i] * Kg[a][j];
           Pn[pidx(i, j)] = v;
         }
@@ -1132,7 +1426,7 @@ struct Solver {
       apply_At(J, k, pc0, t0);
       apply_At(J, k, p1, t1);
       for (int i = 0; i < NX; ++i) {
-        T v0 = W(k, WF::G0 + i) + t0[i], v1 = W(k, WF::G1 + i) + t1[i];
+        T v0 = Gq(k, i) + t0[i], v1 = W(k, WF::G1 + i) + t1[i];
         for (int a = 0; a < NU; ++a) { v0 += Sh[a][i] * k0[a]; v1 += Sh[a][i] * k1[a]; }
         pn0[i] = v0;
         pn1[i] = v1;
@@ -1151,31 +1445,109 @@ struct Solver {
     return true;
   }
 
+  // ---------------- second-order correction: the vector part of the Riccati recursion ----------------
+  // IPOPT's SOC solves the Newton system with the stored factorisation and the constraint right-hand
+  // sides replaced by c_soc (dynamics rows, field SC) and r_soc (the rows' d - s, field SR): only the
+  // stage gradients' row terms a D (d - s) (D = Sigma_s + delta) change, so the costate vector p and the
+  // feed-forward k are recomputed (P, K, the Q_uu factor are the factorisation's):
+  //   pc = P_{k+1} c_k + p_{k+1},  r = g_u + B^T pc,  k = -Q_uu^-1 r,  p_k = g_x + A^T pc + K^T r.
+  MR_HD void soc_backward() {
+    T pv[NX];
+    const T dl = delta_it;
+    // the stage gradient with the SOC's row residuals
+    auto gsoc = [&](int k, T* g) {
+      for (int i = 0; i < NZ; ++i) g[i] = W(k, WF::G0 + i) + mu * W(k, WF::G1 + i) + dl * W(k, WF::GD + i);
+      T z[NZS];
+      load_z(k, cur, z);
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      T d[NI];
+      int act[NI];
+      Row<T> rows[NROW];
+      row_values(k, z, e, d, act, rows);
+      for (int r = 0; r <= NROW; ++r) {
+        const int j0 = r < NROW ? 2 * r : JL, j1 = j0 + 1;
+        if (!act[j0]) continue;
+        int idx[3];
+        T a[3];
+        const int na = row_grad(r, rows, e, idx, a);
+        const T t0 = W(k, sf(cur) + j0), t1 = W(k, sf(cur) + j1);
+        const T s0 = W(k, WF::LAM + j0) / t0, s1 = W(k, WF::LAM + j1) / t1;
+        T dg;  // sum over the rows on a of D (r_soc - r)
+        if (r < 2) {
+          const T r0 = d[j0] - t0, r1 = -(d[j1] - t1);
+          dg = (s0 + dl) * (W(k, WF::SR + j0) - r0) + (s1 + dl) * (W(k, WF::SR + j1) - r1);
+        } else {
+          dg = (s0 + s1 + dl) * (W(k, WF::SR + j0) - (d[j0] - t0));
+        }
+        for (int q = 0; q < na; ++q) g[idx[q]] += a[q] * dg;
+      }
+    };
+    T g[NZ];
+    gsoc(N, g);
+    for (int i = 0; i < NX; ++i) { pv[i] = g[i]; W(N, WF::SPV + i) = pv[i]; }
+    for (int k = N - 1; k >= 0; --k) {
+      T J[48];
+      for (int i = 0; i < 48; ++i) J[i] = W(k, WF::J + i);
+      gsoc(k, g);
+      T pc[NX];
+      for (int i = 0; i < NX; ++i) {
+        T acc = pv[i];
+        for (int l = 0; l < NX; ++l) acc += W(k + 1, WF::P + pidx(i, l)) * W(k, WF::SC + l);
+        pc[i] = acc;
+      }
+      T r[NU];
+      apply_Bt(J, k, pc, r);
+      for (int a = 0; a < NU; ++a) r[a] += g[NX + a];
+      T L[6];
+      for (int q = 0; q < 6; ++q) L[q] = W(k, WF::LQ + q);
+      T kf[NU] = {-r[0], -r[1], -r[2]};
+      chol3_solve(L, kf);
+      for (int a = 0; a < NU; ++a) W(k, WF::SK0 + a) = kf[a];
+      T at[NX];
+      apply_At(J, k, pc, at);
+      for (int i = 0; i < NX; ++i) {
+        T v = g[i] + at[i];
+        for (int a = 0; a < NU; ++a) v += W(k, WF::K + a * NX + i) * r[a];
+        pv[i] = v;
+        W(k, WF::SPV + i) = v;
+      }
+    }
+  }
+
   // ---------------- sweep 3: forward substitution, slack/dual steps ----------------
-  // fraction-to-boundary primal/dual step and the directional derivative of phi_mu
-  MR_HD void forward(T& ap, T& ad, T& gphi) {
+  // The search direction from the factorisation (soc = false: fields DZ, DS, DLAM, DY, DNU) or of a
+  // second-order correction (soc = true: the vector part SK0 / SPV and the right-hand sides SC / SR,
+  // into SDZ, SDS, SDLAM, SDY, SDNU).  Returns the fraction-to-boundary primal / dual step sizes and the
+  // directional derivative of the barrier objective (regular direction).
+  MR_HD void forward(T& ap, T& ad, T& gphi, bool soc = false) {
     const T tau = mr_max(T(0.99), T(1) - mu);
+    const T dl = delta_it, kd = T(IP_KAPPA_D);
+    const int fDZ = soc ? WF::SDZ : WF::DZ, fDS = soc ? WF::SDS : WF::DS, fDL = soc ? WF::SDLAM : WF::DLAM,
+              fDY = soc ? WF::SDY : WF::DY, fDN = soc ? WF::SDNU : WF::DNU;
     ap = T(1);
     ad = T(1);
     gphi = T(0);
     T dx[NX];
     for (int i = 0; i < NX; ++i) dx[i] = T(0);
     if (!MR_KKT_RESTATED && !resto)  // the initial-state rows' multiplier step: stage 0's costate (dx_0 = 0)
-      for (int i = 0; i < NX; ++i) W(0, WF::DNU + i) = W(0, WF::PV0 + i) + mu * W(0, WF::PV1 + i);
+      for (int i = 0; i < NX; ++i)
+        W(0, fDN + i) = soc ? W(0, WF::SPV + i) : W(0, WF::PV0 + i) + mu * W(0, WF::PV1 + i);
     T z[NZS];
     for (int k = 0; k <= N; ++k) {
       T dz[NZS];
       for (int i = 0; i < NX; ++i) dz[i] = dx[i];
       if (k < N) {
         for (int a = 0; a < NU; ++a) {
-          T v = W(k, WF::K0 + a) + mu * W(k, WF::K1 + a);
+          T v = soc ? W(k, WF::SK0 + a) : W(k, WF::K0 + a) + mu * W(k, WF::K1 + a);
           for (int j = 0; j < NX; ++j) v += W(k, WF::K + a * NX + j) * dx[j];
           dz[NX + a] = v;
         }
       } else {
         dz[11] = dz[12] = dz[13] = T(0);
       }
-      for (int i = 0; i < NZ; ++i) gphi += W(k, WF::GL + i) * dz[i];
+      if (!soc)
+        for (int i = 0; i < NZ; ++i) gphi += W(k, WF::GL + i) * dz[i];
       // rows
       load_z(k, cur, z);
       Err<T> e;
@@ -1192,47 +1564,85 @@ struct Solver {
         adz[2 * r + 1] = -v;
       }
       dz[14] = T(0);
+      adz[JL] = adz[JL + 1] = adz[JL + 2] = T(0);
       if (lane_active(P, k)) {
         const T gdz = e.gC[0] * dz[0] + e.gC[1] * dz[1] + e.gC[2] * dz[6];
         adz[JL] = gdz;
         adz[JL + 1] = -gdz;
-        adz[JL + 2] = T(0);
       }
-      for (int i = 0; i < NZS; ++i) W(k, WF::DZ + i) = dz[i];
-      for (int j = 0; j < NI; ++j) {
-        if (!act[j]) continue;
-        T s = W(k, sf(cur) + j), lam = W(k, WF::LAM + j);
-        T ds, dl;
-        if (resto) {
+      for (int i = 0; i < NZS; ++i) W(k, fDZ + i) = dz[i];
+      if (resto) {
+        for (int j = 0; j < NI; ++j) {
+          if (!act[j]) continue;
+          T s = W(k, sf(cur) + j), lam = W(k, WF::LAM + j);
+          T ds, dlv;
           const T p = W(k, WF::RP + j), n = W(k, WF::RN + j), vp = W(k, WF::RVP + j), vn = W(k, WF::RVN + j);
           T dp, dn, dvp, dvn;
-          row_steps_r(adz[j] + (d[j] - s - p + n), s, lam, p, n, vp, vn, rho, mu, ds, dp, dn, dl, dvp, dvn);
+          row_steps_r(adz[j] + (d[j] - s - p + n), s, lam, p, n, vp, vn, rho, mu, ds, dp, dn, dlv, dvp, dvn);
           W(k, WF::RDP + j) = dp;
           W(k, WF::RDN + j) = dn;
           W(k, WF::RDVP + j) = dvp;
           W(k, WF::RDVN + j) = dvn;
-          W(k, WF::RDY + j) = lam + dl - W(k, WF::RY + j);  // eta - y
+          W(k, WF::RDY + j) = lam + dlv - W(k, WF::RY + j);  // eta - y
           gphi += (rho - mu / p) * dp + (rho - mu / n) * dn;
           if (dp < T(0)) ap = mr_min(ap, -tau * p / dp);
           if (dn < T(0)) ap = mr_min(ap, -tau * n / dn);
           if (dvp < T(0)) ad = mr_min(ad, -tau * vp / dvp);
           if (dvn < T(0)) ad = mr_min(ad, -tau * vn / dvn);
-        } else {
-          ds = adz[j] + (d[j] - s);
-          dl = mu / s - lam - (lam / s) * ds;
+          W(k, WF::DS + j) = ds;
+          W(k, WF::DLAM + j) = dlv;
+          gphi -= mu * ds / s;
+          if (ds < T(0)) ap = mr_min(ap, -tau * s / ds);
+          if (dlv < T(0)) ad = mr_min(ad, -tau * lam / dlv);
         }
-        W(k, WF::DS + j) = ds;
-        W(k, WF::DLAM + j) = dl;
-        gphi -= mu * ds / s;
-        if (ds < T(0)) ap = mr_min(ap, -tau * s / ds);
-        if (dl < T(0)) ad = mr_min(ad, -tau * lam / dl);
+      } else {
+        // IPOPT's rows: the slack step ds = a.dz + (d - s) of each row (r_soc for a correction), the
+        // distance steps (upper distance of a two-sided row: -ds), the bound-dual steps
+        // dv = mu/t - v - (v/t) dt, the multiplier step dy = (Sigma_s + delta) ds + grad_s phi - y
+        T t[NI];
+        for (int j = 0; j < NI; ++j) t[j] = act[j] ? W(k, sf(cur) + j) : T(1);
+        for (int r = 0; r <= NROW; ++r) {
+          const int j0 = r < NROW ? 2 * r : JL, j1 = j0 + 1;
+          if (!act[j0]) continue;
+          const T l0 = W(k, WF::LAM + j0), l1 = W(k, WF::LAM + j1);
+          const T s0 = l0 / t[j0], s1 = l1 / t[j1];
+          T dt0, dt1;
+          if (r < 2) {
+            const T R0 = soc ? W(k, WF::SR + j0) : d[j0] - t[j0];
+            const T R1 = soc ? W(k, WF::SR + j1) : -(d[j1] - t[j1]);
+            const T Ds0 = adz[j0] + R0, Ds1 = -adz[j1] + R1;  // IPOPT's slack steps of the two rows
+            dt0 = Ds0;
+            dt1 = -Ds1;
+            W(k, fDY + j0) = (s0 + dl) * Ds0 - mu / t[j0] + kd * mu - W(k, WF::Y + j0);
+            W(k, fDY + j1) = (s1 + dl) * Ds1 + mu / t[j1] - kd * mu - W(k, WF::Y + j1);
+            if (!soc) gphi += kd * mu * (dt0 + dt1);
+          } else {
+            const T R0 = soc ? W(k, WF::SR + j0) : d[j0] - t[j0];
+            const T Ds = adz[j0] + R0;
+            dt0 = Ds;
+            dt1 = -Ds;
+            W(k, fDY + j0) = (s0 + s1 + dl) * Ds - mu / t[j0] + mu / t[j1] - W(k, WF::Y + j0);
+            W(k, fDY + j1) = T(0);
+          }
+          const T dts[2] = {dt0, dt1};
+          for (int sd = 0; sd < 2; ++sd) {
+            const int j = j0 + sd;
+            const T lam = sd ? l1 : l0, dtj = dts[sd];
+            const T dlv = mu / t[j] - lam - (lam / t[j]) * dtj;
+            W(k, fDS + j) = dtj;
+            W(k, fDL + j) = dlv;
+            if (!soc) gphi -= mu * dtj / t[j];
+            if (dtj < T(0)) ap = mr_min(ap, -tau * t[j] / dtj);
+            if (dlv < T(0)) ad = mr_min(ad, -tau * lam / dlv);
+          }
+        }
       }
       if (k < N) {
-        T J[48], t[NX], tb[NX];
+        T J[48], tt[NX], tb[NX];
         for (int i = 0; i < 48; ++i) J[i] = W(k, WF::J + i);
-        apply_A(J, k, dx, t);
+        apply_A(J, k, dx, tt);
         apply_B(J, k, dz + NX, tb);
-        for (int i = 0; i < NX; ++i) dx[i] = t[i] + tb[i] + W(k, WF::C + i);
+        for (int i = 0; i < NX; ++i) dx[i] = tt[i] + tb[i] + (soc ? W(k, WF::SC + i) : W(k, WF::C + i));
         if (resto) {  // + the disturbance of the relaxed vehicle rows, w = -M^-1 (nu_y + gw)
           T Pn[NP], sw[6], rhs[6], w[6];
           for (int i = 0; i < NP; ++i) Pn[i] = W(k + 1, WF::P + i);
@@ -1261,61 +1671,70 @@ struct Solver {
         }
         // multiplier step dnu_{k+1} = P_{k+1} dx_{k+1} + p_{k+1} (correction form, eval_sweep)
         for (int i = 0; i < NX; ++i) {
-          T v = W(k + 1, WF::PV0 + i) + mu * W(k + 1, WF::PV1 + i);
+          T v = soc ? W(k + 1, WF::SPV + i) : W(k + 1, WF::PV0 + i) + mu * W(k + 1, WF::PV1 + i);
           for (int l = 0; l < NX; ++l) v += W(k + 1, WF::P + pidx(i, l)) * dx[l];
-          W(k + 1, WF::DNU + i) = v;  // correction form: the multiplier step itself
+          W(k + 1, fDN + i) = v;  // correction form: the multiplier step itself
         }
       }
     }
   }
+  // the accepted second-order correction becomes the iteration's search direction
+  MR_HD void soc_commit() {
+    for (int k = 0; k <= N; ++k) {
+      for (int i = 0; i < NZS; ++i) W(k, WF::DZ + i) = W(k, WF::SDZ + i);
+      for (int j = 0; j < NI; ++j) {
+        W(k, WF::DS + j) = W(k, WF::SDS + j);
+        W(k, WF::DLAM + j) = W(k, WF::SDLAM + j);
+        W(k, WF::DY + j) = W(k, WF::SDY + j);
+      }
+      for (int i = 0; i < NX; ++i) W(k, WF::DNU + i) = W(k, WF::SDNU + i);
+    }
+  }
 
   // ---------------- sweep 4: line-search trial point ----------------
-  // Writes the trial iterate into buffer 1-cur; returns false if a slack is not positive.
-  MR_HD bool trial(T alpha, bool soc, T& th_t, T& ph_t) {
+  // Writes the trial iterate (along the direction, or the SOC direction) into buffer 1-cur; returns
+  // false if a slack is not positive or a value is not finite.  acc >= 0: accumulate the trial's
+  // constraint values into the second-order correction's right-hand sides, SC = acc SC + c(trial),
+  // SR = acc SR + (d - s)(trial) (IPOPT's c_soc update).
+  MR_HD bool trial(T alpha, bool soc, T& th_t, T& ph_t, T acc = T(-1)) {
     const int nb = 1 - cur;
+    const int fDZ = soc ? WF::SDZ : WF::DZ, fDS = soc ? WF::SDS : WF::DS;
     th_t = T(0);
-    T fv = T(0), lg = T(0), lgr = T(0), tho = T(0), fo = T(0);  // lgr, tho, fo: restoration phase only
-    T z[NZS], zt[NZS], zpl[NZS], zroll[NX];
+    T fv = T(0), lg = T(0), lgr = T(0), tho = T(0), fo = T(0), lin = T(0);  // lgr, tho, fo: restoration only
+    T z[NZS], zt[NZS];
     bool ok = true;
     for (int k = 0; k <= N; ++k) {
       load_z(k, cur, z);
-      for (int i = 0; i < NZS; ++i) zt[i] = z[i] + alpha * W(k, WF::DZ + i);
+      for (int i = 0; i < NZS; ++i) zt[i] = z[i] + alpha * W(k, fDZ + i);
       if (k == 0)
         for (int i = 0; i < NX; ++i) zt[i] = z[i];  // x_0 fixed
       if (k == N) { zt[11] = zt[12] = zt[13] = T(0); }
-      for (int i = 0; i < NZS; ++i) zpl[i] = zt[i];
-      if (soc && k >= 1)
-        for (int i = 0; i < NX; ++i) zt[i] = zroll[i];
-      // rows: slack trial s + alpha ds (+ SOC shift d(z_soc) - d(z_plain))
-      Err<T> e, ep;
+      Err<T> e;
       errors(I, zt[0], zt[1], zt[6], e, false);
-      T d[NI], dp[NI];
+      T d[NI];
       int act[NI];
       Row<T> rows[NROW];
       row_values(k, zt, e, d, act, rows);
-      if (soc) {
-        errors(I, zpl[0], zpl[1], zpl[6], ep, false);
-        int actp[NI];
-        Row<T> rowsp[NROW];
-        row_values(k, zpl, ep, dp, actp, rowsp);
-      }
-      T dyn = T(0);  // this stage's share of theta not from rows (the dynamics defect)
+      T stv[NI];
       for (int j = 0; j < NI; ++j) {
+        stv[j] = T(1);
         if (!act[j]) continue;
-        T st = W(k, sf(cur) + j) + alpha * W(k, WF::DS + j);
-        if (soc) st += d[j] - dp[j];
+        T st = W(k, sf(cur) + j) + alpha * W(k, fDS + j);
         if (!(st > T(0))) ok = false;
+        stv[j] = st;
         W(k, sf(nb) + j) = st;
         lg += mr_log(st > T(0) ? st : T(1));
+        if (oneslot(j)) lin += st;
         if (resto) {
           const T pt = W(k, WF::RP + j) + alpha * W(k, WF::RDP + j), nt = W(k, WF::RN + j) + alpha * W(k, WF::RDN + j);
           if (!(pt > T(0)) || !(nt > T(0))) ok = false;
           th_t += mr_abs(d[j] - st - pt + nt);
-          tho += mr_abs(d[j] - st);
+          if (yslot(j)) tho += mr_abs(d[j] - st);
           lgr += mr_log(pt > T(0) ? pt : T(1)) + mr_log(nt > T(0) ? nt : T(1));
           fv += rho * (pt + nt);
-        } else {
+        } else if (yslot(j)) {
           th_t += mr_abs(d[j] - st);
+          if (acc >= T(0)) W(k, WF::SR + j) = acc * W(k, WF::SR + j) + T(slot_sign(j)) * (d[j] - st);
         }
       }
       if (resto) {
@@ -1329,33 +1748,28 @@ struct Solver {
       if (k < N) {
         T xn[NX];
         faug<T, MODEL>(P, k, zt, xn);
-        if (soc) {
-          for (int i = 0; i < NX; ++i) zroll[i] = xn[i];
-        } else {
-          for (int i = 0; i < NX; ++i) {
-            T xt = W(k + 1, zf(cur) + i) + alpha * W(k + 1, WF::DZ + i);
-            T rel = T(0);
-            if (resto && i < 6) {  // the relaxed vehicle rows
-              const T pt = W(k, WF::CP + i) + alpha * W(k, WF::CDP + i), nt = W(k, WF::CN + i) + alpha * W(k, WF::CDN + i);
-              if (!(pt > T(0)) || !(nt > T(0))) ok = false;
-              rel = nt - pt;
-              lgr += mr_log(pt > T(0) ? pt : T(1)) + mr_log(nt > T(0) ? nt : T(1));
-              fv += rho * (pt + nt);
-              tho += mr_abs(xn[i] - xt);
-            }
-            dyn += mr_abs(xn[i] - xt + rel);
-            if (resto && i >= 6) tho += mr_abs(xn[i] - xt);
+        for (int i = 0; i < NX; ++i) {
+          T xt = W(k + 1, zf(cur) + i) + alpha * W(k + 1, fDZ + i);
+          T rel = T(0);
+          if (resto && i < 6) {  // the relaxed vehicle rows
+            const T pt = W(k, WF::CP + i) + alpha * W(k, WF::CDP + i), nt = W(k, WF::CN + i) + alpha * W(k, WF::CDN + i);
+            if (!(pt > T(0)) || !(nt > T(0))) ok = false;
+            rel = nt - pt;
+            lgr += mr_log(pt > T(0) ? pt : T(1)) + mr_log(nt > T(0) ? nt : T(1));
+            fv += rho * (pt + nt);
           }
+          th_t += mr_abs(xn[i] - xt + rel);
+          tho += mr_abs(xn[i] - xt);
+          if (acc >= T(0) && !resto) W(k, WF::SC + i) = acc * W(k, WF::SC + i) + (xn[i] - xt);
         }
       }
-      th_t += dyn;
-      if (!resto) tho += dyn;
       store_z(k, nb, zt);
     }
-    ph_t = fv - mu * (lg + lgr);
+    const T kdm = T(IP_KAPPA_D) * mu;
+    ph_t = fv - mu * (lg + lgr) + kdm * lin;
     if (resto) {  // the point measured as the original problem sees it (restoration exit test)
       tho_acc = tho;
-      pho_acc = fo - mu_o * lg;
+      pho_acc = fo - mu_o * lg + T(IP_KAPPA_D) * mu_o * lin;
     }
     if (!(th_t == th_t) || !(ph_t == ph_t)) ok = false;
     return ok;
@@ -1367,14 +1781,16 @@ struct Solver {
     return true;
   }
   MR_HD void filter_add(T th, T ph) {
+    const T g_th = T(1e-5), g_ph = T(1e-5);
+    const T a = (T(1) - g_th) * th, b = ph - g_ph * th;
     if (nfilt < FMAX) {
-      filt_th[nfilt] = th;
-      filt_ph[nfilt] = ph;
+      filt_th[nfilt] = a;
+      filt_ph[nfilt] = b;
       nfilt++;
     } else {  // drop the oldest entry
       for (int i = 0; i < FMAX - 1; ++i) { filt_th[i] = filt_th[i + 1]; filt_ph[i] = filt_ph[i + 1]; }
-      filt_th[FMAX - 1] = th;
-      filt_ph[FMAX - 1] = ph;
+      filt_th[FMAX - 1] = a;
+      filt_ph[FMAX - 1] = b;
     }
   }
 
@@ -1385,43 +1801,111 @@ struct Solver {
     return v;
   }
 
-  // Filter backtracking line search (Waechter & Biegler 2006; IPOPT's order of tests): alpha = a0,
-  // a0/2, ... down to a_min, one second-order correction after the first rejected trial when it did
-  // not decrease theta; acceptance = theta_max, then the switching / Armijo or sufficient-decrease
-  // test against (th, ph, gphi), then the filter.  The accepted trial is in buffer 1-cur.  nls counts
-  // the halvings (in/out).
-  MR_HD bool backtrack(T a0, T ap, T th, T ph, T gphi, T a_min, T th_pow, T& alpha, bool& ftype, bool& rej_filter,
-                       int& nls) {
-    const T s_phi = T(2.3), delta_sw = T(1), eta = T(1e-4), g_th = T(1e-5), g_ph = T(1e-5);
-    (void)ap;
-    alpha = a0;
-    const int nls0 = nls;
-    // backtracking ends below a_min, or below 1e-30: a_min is 0 when theta is (and may flush to 0
-    // in fp32), and halving alpha to 0 would never leave the loop
-    while (alpha >= a_min && alpha >= T(1e-30)) {
-      for (int pass = 0; pass < 2; ++pass) {
-        bool soc = pass == 1;
-        T th_t, ph_t;
-        bool ok;
-        MR_PROF(3, ok = trial(alpha, soc, th_t, ph_t));
-        if (ok) ok = th_t <= theta_max;
-        if (ok) {
-          bool sw = gphi < T(0) && alpha * mr_exp(s_phi * mr_log(-gphi)) > delta_sw * th_pow;
-          if (th <= theta_min && sw) {
-            ok = ph_t <= ph + eta * alpha * gphi + T(1e-14) * mr_abs(ph);
-            ftype = true;
-          } else {
-            ok = th_t <= (T(1) - g_th) * th || ph_t <= ph - g_ph * th + T(1e-14) * mr_abs(ph);
-            ftype = false;
-          }
+  // FilterLSAcceptor's tests (IPOPT: Compare_le with 10 eps |reference|, obj_max_inc 5)
+  static MR_HD bool cmp_le(T lhs, T rhs, T bas) { return lhs - rhs <= T(10) * mr_eps<T>() * mr_abs(bas); }
+  MR_HD bool is_ftype(T a_test, const LSRef<T>& r) const {
+    return r.gphi < T(0) && a_test * mr_exp(T(2.3) * mr_log(-r.gphi)) > r.thpow;
+  }
+  MR_HD bool armijo(T ph_t, T a_test, const LSRef<T>& r) const {
+    return cmp_le(ph_t - r.ph, T(1e-4) * a_test * r.gphi, r.ph);
+  }
+  MR_HD bool acc_to_iterate(T th_t, T ph_t, const LSRef<T>& r) const {
+    if (ph_t > r.ph) {
+      const T bas = mr_abs(r.ph) > T(10) ? mr_log(mr_abs(r.ph)) / mr_log(T(10)) : T(1);
+      if (mr_log(ph_t - r.ph) / mr_log(T(10)) > T(IP_OBJ_MAX_INC) + bas) return false;
+    }
+    const T g = T(1e-5);
+    return cmp_le(th_t, (T(1) - g) * r.th, r.th) || cmp_le(ph_t - r.ph, -g * r.th, r.ph);
+  }
+  MR_HD bool acceptable_point(T th_t, T ph_t, T a_test, const LSRef<T>& r) {
+    if (!(th_t <= theta_max)) return false;
+    bool ok;
+    if (a_test > T(0) && is_ftype(a_test, r) && r.th <= theta_min) ok = armijo(ph_t, a_test, r);
+    else ok = acc_to_iterate(th_t, ph_t, r);
+    if (!ok) return false;
+    if (!filter_ok(th_t, ph_t)) { rej_filter = true; return false; }
+    return true;
+  }
+  MR_HD T alpha_min_of(T th, T gphi) const {
+    T a = T(1e-5);
+    if (gphi < T(0)) {
+      a = mr_min(a, T(1e-5) * th / (-gphi));
+      if (th <= theta_min) a = mr_min(a, mr_exp(T(1.1) * mr_log(mr_max(th, T(1e-300)))) / mr_exp(T(2.3) * mr_log(-gphi)));
+    }
+    return T(0.05) * a;
+  }
+
+  // TrySecondOrderCorrection: up to max_soc linear corrections on the stored factorisation, while
+  // theta falls by kappa_soc; the first trial point (alpha a_trial, theta th_trial) is in buffer 1-cur.
+  // On success the SOC direction is the iteration's (soc_commit) and its trial point is in 1-cur.
+  MR_HD bool try_soc(T a_trial, T th_trial, T a_test, const LSRef<T>& ref, T& alpha, T& ph_acc) {
+    // c_soc = c(x_k), r_soc = (d - s)(x_k); then c_soc = a c_soc + c(trial)
+    for (int k = 0; k <= N; ++k) {
+      for (int i = 0; i < NX; ++i) W(k, WF::SC + i) = k < N ? W(k, WF::C + i) : T(0);
+      T z[NZS];
+      load_z(k, cur, z);
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      T d[NI], t[NI];
+      int act[NI];
+      Row<T> rows[NROW];
+      row_values(k, z, e, d, act, rows);
+      for (int j = 0; j < NI; ++j) {
+        t[j] = act[j] ? W(k, sf(cur) + j) : T(1);
+        W(k, WF::SR + j) = (act[j] && yslot(j)) ? T(slot_sign(j)) * (d[j] - t[j]) : T(0);
+      }
+    }
+    T a_soc = a_trial, th_old = T(0), dum, dum2;
+    bool plain = true;  // the trial point to accumulate: the plain first trial, then each SOC trial
+    for (int count = 0; count < IP_MAX_SOC; ++count) {
+      if (count > 0 && !(th_trial <= T(IP_KAPPA_SOC) * th_old)) break;
+      th_old = th_trial;
+      // accumulate the last trial point's constraint values (re-evaluated at a_soc along its direction)
+      trial(a_soc, !plain, dum, dum2, a_soc);
+      soc_backward();
+      T ap_s, ad_s, gd;
+      forward(ap_s, ad_s, gd, true);
+      T th_t, ph_t;
+      const bool fin = trial(ap_s, true, th_t, ph_t);
+      plain = false;
+      a_soc = ap_s;
+      if (!fin) break;
+      if (acceptable_point(th_t, ph_t, a_test, ref)) {
+        alpha = ap_s;
+        ph_acc = ph_t;
+        soc_commit();
+        return true;
+      }
+      th_trial = th_t;
+    }
+    return false;
+  }
+
+  // DoBacktrackingLineSearch: alpha = a_max, a_max/2, ... while alpha > a_min (the first trial always;
+  // skip_first: from a_max/2); in the watchdog one trial point only, judged at the watchdog's step size;
+  // a second-order correction after the first trial when it did not decrease theta.  The accepted
+  // point is in buffer 1-cur.
+  MR_HD bool backtrack(T a_max, bool skip_first, bool in_wd, T wd_atest, const LSRef<T>& ref, T a_min, T& alpha,
+                       T& a_test, T& ph_acc, int& nls, bool& soc_taken) {
+    alpha = skip_first ? T(0.5) * a_max : a_max;
+    nls = skip_first ? 1 : 0;
+    soc_taken = false;
+    for (int n = 0; n < IP_LS_MAX; ++n) {
+      if (!(alpha > a_min || n == 0)) break;
+      a_test = in_wd ? wd_atest : alpha;
+      T th_t, ph_t;
+      bool fin;
+      MR_PROF(3, fin = trial(alpha, false, th_t, ph_t));
+      if (fin && acceptable_point(th_t, ph_t, a_test, ref)) { ph_acc = ph_t; return true; }
+      if (in_wd) break;
+      if (fin && alpha == a_max && !skip_first && theta <= th_t && !resto) {
+        T as, pa;
+        if (try_soc(alpha, th_t, a_test, ref, as, pa)) {
+          alpha = as;
+          ph_acc = pa;
+          soc_taken = true;
+          return true;
         }
-        // the filter last (IPOPT's order: theta_max, sufficient decrease, then the filter), so a
-        // rejection by the filter itself is known for the reset heuristic
-        if (ok && !filter_ok(th_t, ph_t)) { ok = false; rej_filter = true; }
-        if (ok) return true;
-        // second-order correction only after the first rejected trial with theta not decreased (not in
-        // the restoration phase: its rows carry the relaxations p, n)
-        if (!(nls == 0 && !soc && th_t >= th) || resto) break;
       }
       alpha *= T(0.5);
       nls++;
@@ -1436,6 +1920,7 @@ struct Solver {
       for (int j = 0; j < NI; ++j) {
         W(k, WF::WSL + j) = W(k, sf(cur) + j); W(k, WF::WLAM + j) = W(k, WF::LAM + j);
         W(k, WF::WDS + j) = W(k, WF::DS + j); W(k, WF::WDLAM + j) = W(k, WF::DLAM + j);
+        W(k, WF::WY + j) = W(k, WF::Y + j); W(k, WF::WDY + j) = W(k, WF::DY + j);
       }
       for (int i = 0; i < NX; ++i) { wnub[k][i] = nub[k][i]; W(k, WF::WDNU + i) = W(k, WF::DNU + i); }
     }
@@ -1446,25 +1931,37 @@ struct Solver {
       for (int j = 0; j < NI; ++j) {
         W(k, sf(cur) + j) = W(k, WF::WSL + j); W(k, WF::LAM + j) = W(k, WF::WLAM + j);
         W(k, WF::DS + j) = W(k, WF::WDS + j); W(k, WF::DLAM + j) = W(k, WF::WDLAM + j);
+        W(k, WF::Y + j) = W(k, WF::WY + j); W(k, WF::DY + j) = W(k, WF::WDY + j);
       }
       for (int i = 0; i < NX; ++i) { nub[k][i] = wnub[k][i]; W(k, WF::DNU + i) = W(k, WF::WDNU + i); }
     }
   }
+  MR_HD void acc_save() {  // IPOPT's backup acceptable iterate (primal part: what the solve returns)
+    for (int k = 0; k <= N; ++k)
+      for (int i = 0; i < NZS; ++i) W(k, WF::AZ + i) = W(k, zf(cur) + i);
+    have_acc = true;
+  }
+  MR_HD void acc_restore() {
+    for (int k = 0; k <= N; ++k)
+      for (int i = 0; i < NZS; ++i) W(k, zf(cur) + i) = W(k, WF::AZ + i);
+  }
 
   // ---------------- the restoration phase (IPOPT's l1 restoration, W&B 2006 sec. 3.3) ----------------
-  // Entered when the filter line search finds no acceptable step at an infeasible point (pr_max > tol).
-  // The restoration NLP relaxes every constraint of the reference NLP: the 6 vehicle dynamics rows of
-  // each stage (F - x' - p + n = 0) and every inequality row (d(z) - s - p + n = 0); the definitional rows
-  // of the restatement (S+ = S + dS, the previous-control copies) are not constraints of the reference:
+  // Entered when the filter line search finds no acceptable step (and the point is not acceptable / not
+  // almost feasible) or when the inertia correction fails.  The restoration NLP relaxes the 6 vehicle
+  // dynamics rows of each stage (F - x' - p + n = 0) and every inequality slot (d(z) - s - p + n = 0);
+  // the definitional rows of the restatement (S+ = S + dS, the previous-control copies) are not
+  // constraints of the reference:
   //   min rho sum (p + n) + zeta/2 sum D^2 (z - z_R)^2,  p, n >= 0,
   // rho = 1000, zeta = sqrt(mu), D = min(1, 1/|z_R|) on the reference's variables; solved by the same
   // IPM (eval / Riccati / forward / filter line search with its own filter and barrier parameter,
   // starting at max(mu, max violation)).  It returns to the original problem at the first accepted
   // step whose point reduces the original theta to <= 0.9 theta(z_R) and is acceptable to the original
-  // filter (augmented with z_R's entry on entering).
+  // filter (augmented with z_R's entry on entering).  (Deviations from IPOPT's restoration phase: the
+  // initial-state rows X_0 = state0, S_0 = s0 stay hard (x_0 is eliminated), each slot of a two-sided
+  // row is relaxed separately, y starts at 0, no inertia shift of the relaxation variables)
   MR_HD void resto_enter(T th, T ph) {
-    const T g_th = T(1e-5), g_ph = T(1e-5);
-    filter_add((T(1) - g_th) * th, ph - g_ph * th);
+    filter_add(th, ph);
     onfilt = nfilt;
     for (int i = 0; i < FMAX; ++i) { ofilt_th[i] = filt_th[i]; ofilt_ph[i] = filt_ph[i]; }
     mu_o = mu;
@@ -1486,9 +1983,11 @@ struct Solver {
       row_values(k, z, e, d, act, rows);
       for (int j = 0; j < NI; ++j) {
         T p = T(1), n = T(1);
+        W(k, WF::RS0 + j) = W(k, sf(cur) + j);
+        W(k, WF::RLAM + j) = W(k, WF::LAM + j);
         if (act[j]) {
           const T c = d[j] - W(k, sf(cur) + j);
-          th_rows += mr_abs(c);
+          if (yslot(j)) th_rows += mr_abs(c);
           resto_pn(c, mu_r, rho, p, n);
         }
         W(k, WF::RP + j) = p;
@@ -1498,13 +1997,8 @@ struct Solver {
         W(k, WF::RDP + j) = W(k, WF::RDN + j) = W(k, WF::RDVP + j) = W(k, WF::RDVN + j) = T(0);
         W(k, WF::RY + j) = W(k, WF::RDY + j) = T(0);  // the rows' equality multipliers start at 0
         W(k, WF::DLAM + j) = T(0);
-#ifndef MR_RESTO_LAMINIT
-#define MR_RESTO_LAMINIT 2
-#endif
-        if (act[j]) {
-          if (MR_RESTO_LAMINIT == 1) W(k, WF::LAM + j) = mr_min(W(k, WF::LAM + j), rho);
-          if (MR_RESTO_LAMINIT == 2) W(k, WF::LAM + j) = mu_r / W(k, sf(cur) + j);
-        }
+        // the slacks' bound duals: the original problem's, but not above rho (RestoIterateInitializer)
+        if (act[j]) W(k, WF::LAM + j) = mr_min(W(k, WF::LAM + j), rho);
       }
       for (int i = 0; i < NX; ++i) { nub[k][i] = 0.0; W(k, WF::DNU + i) = T(0); }
       if (k < N)
@@ -1536,16 +2030,51 @@ struct Solver {
     return true;
   }
   MR_HD void resto_exit() {
-    // bound multipliers: a Newton step for complementarity at the new point (mu/s), reset to 1 where it
-    // changes them by more than bound_mult_reset_threshold; equality multipliers reset to 0
-    // (constr_mult_reset_threshold = 0); IPOPT's barrier parameter, filter and perturbation state back
+    // a two-sided row's slot distances were relaxed separately: one slack again (distances rescaled to
+    // the row's range).  Bound duals: the whole restoration taken as one primal Newton step for
+    // complementarity at the entry point, dv = mu/t0 - v0 - v0/t0 (t - t0), with the dual fraction to the
+    // boundary; all reset to 1 if one exceeds bound_mult_reset_threshold (1000); y = 0
+    // (constr_mult_reset_threshold 0); IPOPT's barrier parameter, filter and perturbation state back
+    const T tau = mr_max(T(0.99), T(1) - mu_o);
+    T ad = T(1), vmax = T(0);
+    for (int k = 0; k <= N; ++k) {
+      T z[NZS];
+      load_z(k, cur, z);
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      T d[NI];
+      int act[NI];
+      Row<T> rows[NROW];
+      row_values(k, z, e, d, act, rows);
+      for (int r = 2; r <= NROW; ++r) {
+        const int j0 = r < NROW ? 2 * r : JL;
+        if (!act[j0]) continue;
+        const T t0 = W(k, sf(cur) + j0), t1 = W(k, sf(cur) + j0 + 1), rng = d[j0] + d[j0 + 1];
+        W(k, sf(cur) + j0) = t0 * rng / (t0 + t1);
+        W(k, sf(cur) + j0 + 1) = t1 * rng / (t0 + t1);
+      }
+      for (int j = 0; j < NI; ++j) {
+        if (!act[j]) continue;
+        const T t0 = W(k, WF::RS0 + j), v0 = W(k, WF::RLAM + j), t = W(k, sf(cur) + j);
+        const T dv = mu_o / t0 - v0 - v0 / t0 * (t - t0);
+        W(k, WF::DLAM + j) = dv;
+        if (dv < T(0)) ad = mr_min(ad, -tau * v0 / dv);
+      }
+    }
+    for (int k = 0; k <= N; ++k)
+      for (int j = 0; j < NI; ++j) {
+        const T v0 = W(k, WF::RLAM + j);
+        if (v0 == T(0)) continue;  // inactive slot
+        const T v = v0 + ad * W(k, WF::DLAM + j);
+        W(k, WF::LAM + j) = v;
+        vmax = mr_max(vmax, mr_abs(v));
+      }
     for (int k = 0; k <= N; ++k) {
       for (int j = 0; j < NI; ++j) {
-        const T s = W(k, sf(cur) + j), lam = W(k, WF::LAM + j) + alpha_d * W(k, WF::DLAM + j);
-        T ln = mu_o / s;
-        if (mr_abs(ln - lam) > T(RESTO_MULT_RESET)) ln = T(1);
-        W(k, WF::LAM + j) = W(k, WF::LAM + j) == T(0) ? T(0) : ln;  // inactive slots stay 0
+        if (vmax > T(RESTO_MULT_RESET) && W(k, WF::RLAM + j) != T(0)) W(k, WF::LAM + j) = T(1);
         W(k, WF::DLAM + j) = T(0);
+        W(k, WF::Y + j) = T(0);
+        W(k, WF::DY + j) = T(0);
       }
       for (int i = 0; i < NX; ++i) { nub[k][i] = 0.0; W(k, WF::DNU + i) = T(0); }
     }
@@ -1559,67 +2088,102 @@ struct Solver {
     resto = false;
   }
 
+  // IPOPT's tiny-step test (tiny_step_tol 10 eps): every component of the step of the reference's
+  // variables (global X, Y, S) and of IPOPT's slacks s below 10 eps relative to (1 + |value|), at a point
+  // with primal infeasibility <= 1e-4.  ymall: also the multipliers' step below tiny_step_y_tol (1e-2).
+  MR_HD bool tiny_step(bool& ysmall) const {
+    if (!(pr_max <= T(1e-4))) return false;
+    const T tt = T(10) * mr_eps<T>();
+    ysmall = true;
+    for (int k = 0; k <= N; ++k) {
+      T z[NZS];
+      load_z(k, cur, z);
+      for (int i = 0; i < NZ; ++i) {
+        if (!delta_var(i) || (k == 0 && i <= 6) || (k == N && i >= NX)) continue;
+        const T org = i == 0 ? I.org[0] : (i == 1 ? I.org[1] : (i == 6 ? I.org[2] : T(0)));
+        if (mr_abs(W(k, WF::DZ + i)) > tt * (T(1) + mr_abs(z[i] + org))) return false;
+      }
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      T d[NI];
+      int act[NI];
+      Row<T> rows[NROW];
+      row_values(k, z, e, d, act, rows);
+      for (int j = 0; j < NI; ++j) {
+        if (!act[j] || !yslot(j)) continue;
+        const T c = j < JL ? rows[j / 2].c : e.eC;
+        const T sv = c - T(slot_sign(j)) * (d[j] - W(k, sf(cur) + j));  // IPOPT's slack value
+        if (mr_abs(W(k, WF::DS + j)) > tt * (T(1) + mr_abs(sv))) return false;
+        if (!(mr_abs(W(k, WF::DY + j)) < T(1e-2))) ysmall = false;
+      }
+      for (int i = 0; i < NX; ++i)
+        if ((i < 6 || (k == 0 && i == 6)) && !(mr_abs(W(k, WF::DNU + i)) < T(1e-2))) ysmall = false;
+    }
+    return true;
+  }
+
   // ---------------- the IPM loop ----------------
   MR_HD SolveOut solve() {
     const T kappa_eps = T(10), kappa_mu = T(0.2), theta_mu = T(1.5);
-    const T mu_min = P.tol / T(10);
-    const T s_phi = T(2.3), s_theta = T(1.1), delta_sw = T(1), eta = T(1e-4), g_th = T(1e-5), g_ph = T(1e-5);
+    // IPOPT's monotone update keeps mu >= min(tol, compl_inf_tol) / (barrier_tol_factor + 1)
+    const T mu_min = mr_max(T(1e-11), mr_min(P.tol, T(IP_COMPL_INF_TOL)) / (kappa_eps + T(1)));
     SolveOut out{2, 0, 0.0, 0.0};
     T mu_prev = mu;
     int acc_count = 0;
-    int ls_fail = 0;  // consecutive iterations without an acceptable line-search step
     // IPOPT's filter reset heuristic (filter_reset_trigger = 5, max_filter_resets = 5): after this many
     // successive iterations whose line search had a trial point rejected by the filter, clear it
     int filt_rej_iters = 0, filt_resets = 0;
     // watchdog state and the reference values of the point where it started
-    bool in_wd = false;
+    bool in_wd = false, tiny_flag = false;
     int wd_short = 0, wd_trial = 0;
-    T wd_th = T(0), wd_ph = T(0), wd_gphi = T(0), wd_ap = T(0), wd_ad = T(0), wd_amin = T(0), wd_thpow = T(0);
+    LSRef<T> wd_ref{T(0), T(0), T(0), T(0)};
+    T wd_ap = T(0), wd_ad = T(0), wd_amin = T(0);
     int it = 0;
     for (it = 0;; ++it) {
       MR_PROF(0, eval_sweep(mu_prev));
-      if (trace && it == 0 && trace_cap >= 100 + N + 1) {  // diagnostics: initial defects per stage
-        for (int k = 0; k < N; ++k) {
-          double* tr = trace + 8 * (100 + k);
-          for (int i = 0; i < 6; ++i) tr[i] = (double)W(k, WF::C + i);
-          tr[6] = (double)(mr_abs(W(k, WF::C + 6)) + mr_abs(W(k, WF::C + 7)) + mr_abs(W(k, WF::C + 8)) +
-                           mr_abs(W(k, WF::C + 9)) + mr_abs(W(k, WF::C + 10)));
-          tr[7] = (double)W(k + 1, zf(cur) + 3);
-        }
-      }
-      T kkt = kkt_error(T(0));
+      T kkt = nlp_error();
       if (!(kkt == kkt) || !(fval == fval)) { out.status = 3; break; }
 #ifdef MR_RESTO_DEBUG
-      if (trace) printf("it %d resto %d kkt %.3e stat %.3e pr %.3e smax %.3e smin %.3e nu1 %.3e lam1 %.3e mi %d mu %.3e fval %.6e theta %.4e\n", it, (int)resto, (double)kkt, (double)stat_max, (double)pr_max, (double)slam_max, (double)slam_min, (double)nu1, (double)lam1, mi, (double)mu, (double)fval, (double)theta);
+      if (trace) printf("it %d resto %d kkt %.3e stat %.3e pr %.3e viol %.3e smax %.3e nu1 %.3e y1 %.3e lam1 %.3e mu %.3e fval %.6e theta %.4e\n", it, (int)resto, (double)kkt, (double)stat_max, (double)pr_max, (double)viol_max, (double)slam_max, (double)nu1, (double)y1, (double)lam1, (double)mu, (double)fval, (double)theta);
+      if (trace) printf("   acc %d conv %d compl/sc %.3e cv %.3e du %.3e tiny %d\n", (int)acceptable(kkt), (int)converged(kkt), (double)(compl_err(T(0)) / sc), (double)mr_max(pr_eq, viol_max), (double)(stat_max / sc), (int)tiny_flag);
 #endif
       if (resto) {
         // the restoration NLP converged at a point the original problem does not accept: IPOPT's
-        // "converged to a point of local infeasibility"
-        if (kkt <= P.tol) { out.status = MR_STATUS_INFEASIBLE; break; }
+        // "restoration converged to a feasible point unacceptable to the filter" (restoration failed)
+        // when that point is feasible to 1e2 tol, else "converged to a point of local infeasibility"
+        if (kkt <= P.tol) { out.status = pr_o <= T(100) * P.tol ? 3 : MR_STATUS_INFEASIBLE; break; }
       } else {
         out.kkt = (double)kkt;
         out.obj = (double)(fval / sc);
-        if (kkt <= P.tol) { out.status = 0; break; }
+        if (converged(kkt)) { out.status = 0; break; }
         if (P.acc_iter > 0) {
-          acc_count = (kkt <= P.acc_tol) ? acc_count + 1 : 0;
+          acc_count = acceptable(kkt) ? acc_count + 1 : 0;
           if (acc_count >= P.acc_iter) { out.status = 1; break; }
         }
       }
       if (it >= P.max_iter) { out.status = 2; break; }
       T mu_old = mu;
-      while (kkt_error(mu) <= kappa_eps * mu && mu > mu_min) {
-        T m1 = kappa_mu * mu, m2 = mr_exp(theta_mu * mr_log(mu));
-        mu = mr_max(mu_min, mr_min(m1, m2));
+      bool mu_stuck = false;
+      while (barrier_error(mu) <= kappa_eps * mu || tiny_flag) {
+        const T m1 = kappa_mu * mu, m2 = mr_exp(theta_mu * mr_log(mu));
+        const T mn = mr_max(mu_min, mr_min(m1, m2));
+        if (mn == mu) { mu_stuck = tiny_flag; break; }
+        mu = mn;
+        tiny_flag = false;
       }
+      if (mu_stuck) { out.status = 3; break; }  // tiny step at the smallest mu (IPOPT: search direction too small)
+      tiny_flag = false;
       if (mu != mu_old) {  // IPOPT resets its line search with a new barrier problem: filter and watchdog
         nfilt = 0;
         in_wd = false;
         wd_short = 0;
       }
-      // inertia-corrected factorisation
+      const T ph_cur = fval - mu * logs + T(IP_KAPPA_D) * mu * lins;  // the barrier objective (+ damping)
+      // inertia-corrected factorisation (PDPerturbationHandler: delta = 0 first; then delta_xs_init 1e-4
+      // or delta_last / 3; x100 while delta_last is 0 or delta > 1e5 delta_last, else x8; up to 1e40)
       T delta = T(0);
       bool first = true, fact_ok = false;
-      for (int tries = 0; tries < 60; ++tries) {
+      for (int tries = 0; tries < 200; ++tries) {
         bool rok;
         MR_PROF(1, rok = riccati(delta));
         if (rok) { fact_ok = true; break; }
@@ -1627,31 +2191,34 @@ struct Solver {
           delta = delta_last == T(0) ? T(1e-4) : mr_max(T(1e-20), delta_last / T(3));
           first = false;
         } else {
-          delta *= (delta_last == T(0) ? T(100) : T(8));
+          delta *= (delta_last == T(0) || T(1e5) * delta_last < delta) ? T(100) : T(8);
         }
         if (delta > T(1e40)) break;
       }
-      if (!fact_ok) { out.status = 3; break; }
+      if (!fact_ok) {
+        if (resto) { out.status = 3; break; }
+        // IPOPT: no inertia-correct factorisation -> the restoration phase
+        resto_enter(theta, ph_cur);
+        mu_prev = mu;
+        in_wd = false;
+        wd_short = 0;
+        acc_count = 0;
+        continue;
+      }
       if (delta > T(0)) delta_last = delta;
+      delta_it = delta;
       T ap, ad, gphi;
       MR_PROF(2, forward(ap, ad, gphi));
       // filter line search
-      T th = theta, ph = fval - mu * logs;
-      T th_pow = mr_exp(s_theta * mr_log(mr_max(th, T(1e-30))));
-      T a_min;
-      if (gphi < T(0)) {
-        T t1 = g_ph * th / (-gphi);
-        T t2 = delta_sw * th_pow / mr_exp(s_phi * mr_log(-gphi));
-        // IPOPT (W&B 2006 eq. 23, CalculateAlphaMin): the switching term only at theta <= theta_min
-        a_min = T(0.05) * mr_min(g_th, th <= theta_min ? mr_min(t1, t2) : t1);
-      } else {
-        a_min = T(0.05) * g_th;
-      }
+      T th = theta, ph = ph_cur;
+      LSRef<T> ref{th, ph, gphi, mr_exp(T(1.1) * mr_log(mr_max(th, T(1e-300))))};
+      const T a_min = alpha_min_of(th, gphi);
+      rej_filter = false;
       if (resto) {  // a restoration-phase step: its own filter, no watchdog, no second-order correction
-        T alpha = ap;
-        bool ftype = false, rej_filter = false;
+        T alpha, a_test, ph_acc;
         int nls = 0;
-        const bool accepted = backtrack(ap, ap, th, ph, gphi, a_min, th_pow, alpha, ftype, rej_filter, nls);
+        bool soc_taken;
+        const bool accepted = backtrack(ap, false, false, T(0), ref, a_min, alpha, a_test, ph_acc, nls, soc_taken);
         if (!accepted) { out.status = 3; break; }  // IPOPT: restoration failed
         for (int k = 0; k <= N; ++k) {
           for (int j = 0; j < NI; ++j) {
@@ -1664,7 +2231,7 @@ struct Solver {
               W(k, WF::CN + i) += alpha * W(k, WF::CDN + i);
             }
         }
-        if (!ftype) filter_add((T(1) - g_th) * th, ph - g_ph * th);
+        if (!(is_ftype(a_test, ref) && armijo(ph_acc, a_test, ref))) filter_add(th, ph);
         if (trace && it < trace_cap) {
           double* tr = trace + 8 * it;
           tr[0] = (double)kkt; tr[1] = (double)mu; tr[2] = (double)alpha; tr[3] = (double)ad;
@@ -1684,49 +2251,70 @@ struct Solver {
         }
         continue;
       }
+      if (acceptable(kkt)) acc_save();  // IPOPT stores the current iterate if it is acceptable
 #if MR_WD_TRIGGER > 0
       // IPOPT's watchdog (watchdog_shortened_iter_trigger, watchdog_trial_iter_max): after that many
       // successive iterations whose accepted step was shorter than the fraction-to-boundary step, store
       // the iterate and its search direction and take full steps tentatively; they are judged against
-      // the stored point, and after watchdog_trial_iter_max iterations without an acceptable one the
-      // solver returns to the stored point and backtracks along its direction (skipping the full step)
+      // the stored point (at its step size), and after watchdog_trial_iter_max iterations without an
+      // acceptable one the solver returns to the stored point and backtracks along its direction
+      // (skipping the full step)
       if (!in_wd && wd_short >= MR_WD_TRIGGER) {
         wd_save();
-        wd_th = th; wd_ph = ph; wd_gphi = gphi; wd_ap = ap; wd_ad = ad; wd_amin = a_min; wd_thpow = th_pow;
+        wd_ref = ref;
+        wd_ap = ap; wd_ad = ad; wd_amin = a_min;
         in_wd = true;
         wd_trial = 0;
       }
 #endif
-      T alpha = ap;
-      bool accepted = false, ftype = false, rej_filter = false, take_anyway = false;
+      T alpha = ap, a_test = ap, ph_acc = ph;
+      bool accepted = false, take_anyway = false, tiny = false, soc_taken = false;
       int nls = 0;
-      if (in_wd) {
-        accepted = backtrack(ap, ap, wd_th, wd_ph, wd_gphi, ap, wd_thpow, alpha, ftype, rej_filter, nls);
+      LSRef<T> used = ref;
+      bool ysmall = false;
+      if (MR_TINY_STEP && tiny_step(ysmall)) {  // IPOPT: a tiny step is taken without line search (and forces a mu decrease)
+        T th_t, ph_t;
+        trial(ap, false, th_t, ph_t);
+        accepted = tiny = true;
+        tiny_flag = ysmall;
+      } else if (in_wd) {
+        accepted = backtrack(ap, false, true, wd_ap, wd_ref, ap, alpha, a_test, ph_acc, nls, soc_taken);
+        used = wd_ref;
         if (accepted) {
           in_wd = false;
           wd_short = 0;
-          th = wd_th; ph = wd_ph;  // the filter entry is the watchdog point's (the acceptor's reference)
         } else if (++wd_trial <= MR_WD_TRIAL_MAX) {
-          take_anyway = true;  // the full step is taken tentatively (its trial is in buffer 1-cur)
+          take_anyway = true;  // the full step is taken tentatively
           alpha = ap;
           T th_t, ph_t;
-          trial(alpha, false, th_t, ph_t);  // (re-)write the plain full-step point (the last trial may be a SOC)
+          trial(alpha, false, th_t, ph_t);
         } else {
           // back to the watchdog point: its iterate and direction, a regular backtracking line search
           // that skips the full step
           wd_restore();
           in_wd = false;
           wd_short = 0;
-          th = wd_th; ph = wd_ph; gphi = wd_gphi; ap = wd_ap; ad = wd_ad; a_min = wd_amin; th_pow = wd_thpow;
-          alpha = T(0.5) * ap;
-          nls = 1;
-          accepted = backtrack(alpha, ap, th, ph, gphi, a_min, th_pow, alpha, ftype, rej_filter, nls);
+          ref = wd_ref;
+          used = wd_ref;
+          ap = wd_ap; ad = wd_ad;
+          accepted = backtrack(ap, true, false, T(0), ref, wd_amin, alpha, a_test, ph_acc, nls, soc_taken);
+          th = ref.th; ph = ref.ph;
         }
       } else {
-        accepted = backtrack(ap, ap, th, ph, gphi, a_min, th_pow, alpha, ftype, rej_filter, nls);
+        accepted = backtrack(ap, false, false, T(0), ref, a_min, alpha, a_test, ph_acc, nls, soc_taken);
       }
-      // no acceptable step at an infeasible point: the restoration phase (from the next iteration on)
-      if (!accepted && !take_anyway && pr_max > P.tol) {
+#ifdef MR_RESTO_DEBUG
+      if (trace) printf("   ls accepted %d take %d tiny %d alpha %.3e ap %.3e amin %.3e soc %d\n", (int)accepted, (int)take_anyway, (int)tiny, (double)alpha, (double)ap, (double)a_min, (int)soc_taken);
+#endif
+      if (!accepted && !take_anyway) {
+        // IPOPT on a failed line search: (the soft restoration phase is not restated here)
+        // the current point acceptable -> "acceptable point reached"; almost feasible (theta <= 1e-2 tol)
+        // -> the stored acceptable point, or restoration failed; otherwise the restoration phase
+        if (acceptable(kkt)) { out.status = 1; break; }
+        if (theta <= T(1e-2) * P.tol) {
+          if (have_acc) { acc_restore(); out.status = 1; } else { out.status = 3; }
+          break;
+        }
         resto_enter(th, ph);
         mu_prev = mu;
         in_wd = false;
@@ -1739,16 +2327,8 @@ struct Solver {
         }
         continue;
       }
-      // no acceptable step at a point feasible to the tolerance: the shortest tried step (see mr_wave.h)
-      ls_fail = (accepted || take_anyway) ? 0 : ls_fail + 1;
-      if (ls_fail >= MR_LS_FAIL_MAX) { out.status = 3; break; }
-      if (!accepted && !take_anyway) {
-        alpha = mr_min(mr_max(alpha, a_min), ap);
-        T th_t, ph_t;
-        trial(alpha, false, th_t, ph_t);
-        ftype = false;
-      }
-      if (!take_anyway) wd_short = (accepted && alpha < ap) ? wd_short + 1 : 0;
+      if (soc_taken) ad = wd_ad_of_commit();
+      if (!take_anyway && !tiny) wd_short = (alpha < ap) ? wd_short + 1 : 0;
 #if MR_FILTER_RESET_TRIGGER > 0
       if (filt_resets < MR_MAX_FILTER_RESETS) {
         filt_rej_iters = rej_filter ? filt_rej_iters + 1 : 0;
@@ -1759,12 +2339,14 @@ struct Solver {
         }
       }
 #endif
-      if (!ftype && !take_anyway) filter_add((T(1) - g_th) * th, ph - g_ph * th);
+      // IPOPT augments the filter unless the step is f-type with the Armijo condition
+      if (!take_anyway && !tiny && !(is_ftype(a_test, used) && armijo(ph_acc, a_test, used)))
+        filter_add(used.th, used.ph);
       if (trace && it < trace_cap) {
         double* tr = trace + 8 * it;
         tr[0] = (double)kkt; tr[1] = (double)mu; tr[2] = (double)alpha; tr[3] = (double)ad;
-        tr[4] = (double)delta; tr[5] = (double)th; tr[6] = (double)ph;
-        tr[7] = (double)(take_anyway ? -100 - wd_trial : (accepted ? nls : -1));
+        tr[4] = (double)delta; tr[5] = (double)used.th; tr[6] = (double)used.ph;
+        tr[7] = (double)(take_anyway ? -100 - wd_trial : (soc_taken ? 100 + nls : nls));
       }
       alpha_p = alpha;
       alpha_d = ad;
@@ -1778,6 +2360,17 @@ struct Solver {
       tr[4] = (double)pr_max; tr[5] = (double)sc; tr[6] = (double)mu; tr[7] = 1000.0 + out.status;
     }
     return out;
+  }
+  // the dual step size of the committed second-order-correction direction (fraction to the boundary)
+  MR_HD T wd_ad_of_commit() const {
+    const T tau = mr_max(T(0.99), T(1) - mu);
+    T ad = T(1);
+    for (int k = 0; k <= N; ++k)
+      for (int j = 0; j < NI; ++j) {
+        const T lam = W(k, WF::LAM + j), dl = W(k, WF::DLAM + j);
+        if (lam != T(0) && dl < T(0)) ad = mr_min(ad, -tau * lam / dl);
+      }
+    return ad;
   }
 };
 

@@ -304,6 +304,54 @@ class MPCProblem:
             out += [eC[1:] + self.max_error + t, self.max_error - eC[1:] + t, t]
         return torch.cat(out)
 
+    # ---- IPOPT's view of the Opti problem (casadi 3.6.5 Opti -> nlpsol 'ipopt') ----
+    def ipopt_ineq(self):
+        """The inequality rows as casadi's Opti hands them to IPOPT: one row per ``subject_to`` call with
+        a constant side moved into the bounds, so ``opti.bounded(lb, e, ub)`` (MPC.py:134, :142-143,
+        :145-149; the lane row :135 when enabled) is ONE row with two finite bounds, while
+        ``U[0, i] < d_max`` and ``U[0, i] > min_throttle`` (MPC.py:138-141) are two separate one-sided
+        rows.  Equality rows are ``g`` (S_0, X_0, the dynamics).  Returns (d(w), dL, dU, kinds) with
+        -inf / +inf for a missing side; the row order is grouped by kind (IPOPT's iterates do not depend
+        on it)."""
+        fp, N, Ts = self.fp, self.N, self.Ts
+        inf = math.inf
+        kinds, lo, hi = [], [], []
+
+        def grp(kind, n, lb, ub):
+            kinds.extend([kind] * n)
+            lo.extend([lb] * n)
+            hi.extend([ub] * n)
+        grp("ds", N, 0.1, Ts * fp.v_max)
+        if self.lane:
+            grp("lane", N, -self.max_error, self.max_error)
+        grp("thr_hi", N, -inf, self.d_max)
+        grp("thr_lo", N, fp.min_throttle, inf)
+        grp("steer_hi", N, -inf, fp.max_steer)
+        grp("steer_lo", N, fp.min_steer, inf)
+        grp("dthr", N, fp.min_throttle_delta, fp.max_throttle_delta)
+        grp("dsteer", N, fp.min_steer_delta, fp.max_steer_delta)
+        st = self.state0
+        has_t, has_s = st.get("throttle") is not None, st.get("steer") is not None
+        if has_t:
+            grp("thr0", 1, fp.min_throttle_delta, fp.max_throttle_delta)
+        if has_s:
+            grp("steer0", 1, fp.min_steer_delta, fp.max_steer_delta)
+
+        def d(w):
+            U, S, X = self.split(w)
+            out = [S[1:] - S[:-1]]
+            if self.lane:
+                eC, _ = self.errors(S, X[0], X[1])
+                out.append(eC[1:])
+            out += [U[0], U[0], U[1], U[1],
+                    U[0] - torch.roll(U[0], 1), U[1] - torch.roll(U[1], 1)]  # Python index i-1: U[:, -1] at i = 0
+            if has_t:
+                out.append((U[0, 0] - st["throttle"]).reshape(1))
+            if has_s:
+                out.append((U[1, 0] - st["steer"]).reshape(1))
+            return torch.cat(out)
+        return d, np.array(lo, dtype=np.float64), np.array(hi, dtype=np.float64), kinds
+
     # ---- the reference's own row order (CasADi Opti call order, MPC.py:101-149) ----
     def opti_rows(self, w):
         """(g, lbg, ubg) in the order the reference's ``subject_to`` calls create them, with
