@@ -990,7 +990,7 @@ struct Solver {
         for (int i = 0; i < NX; ++i) dx[i] = t[i] + tb[i];
       }
     }
-    if (!(ok == ok) || !ok)
+    if (!ok)
       for (int k = 0; k <= N; ++k) {
         for (int i = 0; i < NX; ++i) nub[k][i] = 0.0;
         for (int j = 0; j < NI; ++j) W(k, WF::Y + j) = T(0);

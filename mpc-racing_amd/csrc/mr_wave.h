@@ -81,16 +81,30 @@ namespace mr {
 struct SSF {
   enum {
     Z0 = 0, Z1 = Z0 + NZS, DZ = Z1 + NZS, S0 = DZ + NZS, S1 = S0 + NI, LAM = S1 + NI, DLAM = LAM + NI,
-    DS = DLAM + NI, DNU = DS + NI, GL = DNU + NX, NF = GL + NZ
+    DS = DLAM + NI, DNU = DS + NI, GL = DNU + NX,
+    Y = GL + NZ, DY = Y + NI,  // IPOPT's row multipliers y_d and their step (mr_solver.h WF::Y)
+    NF = DY + NI
   };
 };
+// The sparse pattern of the inertia correction's slack shift (mr_solver.h HD): sum over a stage's rows of
+// a a^T -- box / rate / wrap rows on (7..13), the lane row on (0, 1, 6); packed upper (i, j) -> slot
+MR_HD constexpr int hd_slot(int i, int j) {
+  return (i == 7 && j == 7) ? 0 : (i == 7 && j == 11) ? 1 : (i == 8 && j == 8) ? 2 : (i == 8 && j == 12) ? 3
+       : (i == 9 && j == 9) ? 4 : (i == 9 && j == 11) ? 5 : (i == 10 && j == 10) ? 6 : (i == 10 && j == 12) ? 7
+       : (i == 11 && j == 11) ? 8 : (i == 12 && j == 12) ? 9 : (i == 13 && j == 13) ? 10 : (i == 0 && j == 0) ? 11
+       : (i == 0 && j == 1) ? 12 : (i == 0 && j == 6) ? 13 : (i == 1 && j == 1) ? 14 : (i == 1 && j == 6) ? 15
+       : (i == 6 && j == 6) ? 16 : -1;
+}
+constexpr int NHD = 17;
 // Stage record (stage-major, RC_STRIDE words per stage): the evaluation sweep's stage QP data
 // (Jacobian, defect, Hessian, gradients), then the Riccati sweep's outputs.
 struct RCF {
   enum {
     J = 0, C = J + 48, H = C + NX, G0 = H + NH, G1 = G0 + NZ,
-    P = G1 + NZ, PV0 = P + NP, K = PV0 + NX, K0 = K + NU * NX,
-    CONE = K0 + NU, CZERO, SELP, SEL0,  // constants 1, 0, [k > 0], [k == 0] (written once per solve)
+    HD = G1 + NZ, GD = HD + NHD,  // the slack shift's pattern (hd_slot) and sum a (d - s) (delta_s)
+    P = GD + NZ, PV0 = P + NP, K = PV0 + NX, K0 = K + NU * NX,
+    LQ = K0 + NU,  // Q_uu's Cholesky factor: L10, L20, L21 and the reciprocal pivots (SOC re-solves)
+    CONE = LQ + 6, CZERO, SELP, SEL0,  // constants 1, 0, [k > 0], [k == 0] (written once per solve)
     JUNK, NF                           // discard slot of the branch-free stores (any lane)
   };
 };
@@ -108,8 +122,12 @@ static_assert(RCF::NF <= RC_STRIDE, "record");
 struct CSF {
   enum {
     WZ = 0, WSL = WZ + NZS, WLAM = WSL + NI, WDZ = WLAM + NI, WDS = WDZ + NZS, WDLAM = WDS + NI,
-    WDNU = WDLAM + NI,
-    RP = WDNU + NX, RN = RP + NI, RVP = RN + NI, RVN = RVP + NI, RDP = RVN + NI, RDN = RDP + NI, RDVP = RDN + NI,
+    WDNU = WDLAM + NI, WY = WDNU + NX, WDY = WY + NI,
+    // second-order corrections: right-hand sides c_soc / r_soc, the direction, the vector pass (g_soc,
+    // costate p, feed-forward k); the restoration entry point; IPOPT's stored acceptable iterate
+    SC = WDY + NI, SR = SC + NX, SG = SR + NI, SPV = SG + NZ, SK0 = SPV + NX, SDZ = SK0 + NU, SDS = SDZ + NZS,
+    SDLAM = SDS + NI, SDY = SDLAM + NI, SDNU = SDY + NI, RS0 = SDNU + NX, RLAM = RS0 + NI, AZ = RLAM + NI,
+    RP = AZ + NZS, RN = RP + NI, RVP = RN + NI, RVN = RVP + NI, RDP = RVN + NI, RDN = RDP + NI, RDVP = RDN + NI,
     RDVN = RDVP + NI, RY = RDVN + NI, RDY = RY + NI, RZ = RDY + NI,
     CP = RZ + NZS, CN = CP + 6, CVP = CN + 6, CVN = CVP + 6, CDP = CVN + 6, CDN = CDP + 6, CDVP = CDN + 6,
     CDVN = CDVP + 6, CSW = CDVN + 6, CGW0 = CSW + 6, CGW1 = CGW0 + 6, NF = CGW1 + 6
@@ -127,9 +145,13 @@ MR_HD constexpr int64_t ws_words() { return WS_NU_OFF + 2 * NX * WL * (int64_t)(
 // solver objects, whose LDS footprint sets the occupancy.
 template <typename T>
 struct WaveCold {
-  int resto, in_wd, wd_short, wd_trial, onfilt;
+  int resto, in_wd, wd_short, wd_trial, onfilt, mrow, have_acc, tiny;
   T rho, zeta, mu_o, th_entry, delta_last_o, theta_max_o, theta_min_o, tho, pho;
   T wd_th, wd_ph, wd_gphi, wd_ap, wd_ad, wd_amin, wd_thpow;
+  // evaluation aggregates beyond the solver object's (mr_solver.h Solver): primal infeasibility of the
+  // equality rows, bound violation of the rows, |y|_1, the damped slacks' sum, the original problem's
+  // primal infeasibility in the restoration phase; the accepted factorisation's delta
+  T pr_eq, viol, y1, lins, pr_o, delta_it;
   T ofilt[2 * FMAX];  // the original problem's filter while the restoration phase runs
 };
 template <typename T>
@@ -169,7 +191,16 @@ MR_HD constexpr int RI(int r, int a) {
 MR_HD constexpr int RS(int a) { return a ? -1 : 1; }
 
 template <typename T>
+MR_HD void row_bounds_raw(const ProbParams<T>& P, const Inst<T>& I, int k, int r, int& act, T& lo, T& hi);
+// the bounds as IPOPT uses them (bound_relax_factor, mr_solver.h relax_amt)
+template <typename T>
 MR_HD void row_bounds(const ProbParams<T>& P, const Inst<T>& I, int k, int r, int& act, T& lo, T& hi) {
+  row_bounds_raw(P, I, k, r, act, lo, hi);
+  lo -= relax_amt(lo);
+  hi += relax_amt(hi);
+}
+template <typename T>
+MR_HD void row_bounds_raw(const ProbParams<T>& P, const Inst<T>& I, int k, int r, int& act, T& lo, T& hi) {
   const int N = P.N;
   act = 0; lo = T(0); hi = T(0);
   if (k == N) return;
@@ -257,7 +288,7 @@ struct WaveSolver {
   int me, mi;
   // out-parameters of the non-inlined sweeps: members, so they land in the object's LDS slot
   // rather than in the caller's private stack (a scratch round trip after every call)
-  T res_ap, res_ad, res_gphi, res_alpha;
+  T res_ap, res_ad, res_gphi, res_alpha, res_th, res_ph, res_atest;
   int res_flags, res_nls, res_ntr, res_nsoc;
   double* trace = nullptr;
   int trace_cap = 0;
@@ -348,23 +379,45 @@ struct WaveSolver {
       T d[NI];
       int act[NI];
       row_values(k, my, e, d, act);
+      // IPOPT's slack push (mr_solver.h Solver::init): one-sided box rows at least 1e-2 max(1, |b|)
+      // inside; a two-sided row's slack s projected into [lo + p_L, hi - p_U]
+      T t[NI];
+#pragma unroll
+      for (int j = 0; j < NI; ++j) t[j] = T(1);
+#pragma unroll
+      for (int r = 0; r <= NROW; ++r) {
+        const int j0 = r < NROW ? 2 * r : JL;
+        if (!act[j0]) continue;
+        int ra;
+        T lo, hi, c;
+        if (r < NROW) {
+          row_bounds(P, I, k, r, ra, lo, hi);
+          c = row_c(r, my);
+        } else {
+          hi = I.max_err + relax_amt(I.max_err);
+          lo = -hi;
+          c = e.eC;
+        }
+        if (r < 2) {
+          t[j0] = mr_max(d[j0], T(1e-2) * mr_max(T(1), mr_abs(lo)));
+          t[j0 + 1] = mr_max(d[j0 + 1], T(1e-2) * mr_max(T(1), mr_abs(hi)));
+        } else {
+          const T rng = hi - lo;
+          const T pL = mr_min(T(1e-2) * mr_max(T(1), mr_abs(lo)), T(1e-2) * rng);
+          const T pU = mr_min(T(1e-2) * mr_max(T(1), mr_abs(hi)), T(1e-2) * rng);
+          const T sv = mr_min(mr_max(c, lo + pL), hi - pU);
+          t[j0] = sv - lo;
+          t[j0 + 1] = hi - sv;
+        }
+      }
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        T push;
-        if (j < JL) {
-          int ra;
-          T lo, hi;
-          row_bounds(P, I, k, j / 2, ra, lo, hi);
-          T bnd = (j & 1) ? mr_abs(hi) : mr_abs(lo);
-          push = mr_min(T(1e-2) * mr_max(T(1), bnd), T(1e-2) * (hi - lo));
-        } else {
-          push = j < JL + 2 ? T(1e-2) * mr_max(T(1), I.max_err) : T(1e-2);
-        }
-        T s = act[j] ? mr_max(d[j], push) : T(1);
-        S(SSF::S0 + j) = s;
+        S(SSF::S0 + j) = t[j];
         S(SSF::LAM + j) = act[j] ? T(1) : T(0);
         S(SSF::DLAM + j) = T(0);
-        if (act[j]) th += mr_abs(d[j] - s);
+        S(SSF::Y + j) = T(0);
+        S(SSF::DY + j) = T(0);
+        if (act[j] && yslot(j)) th += mr_abs(d[j] - t[j]);
       }
       for (int i = 0; i < NX; ++i) { NUd(i) = 0.0; S(SSF::DNU + i) = T(0); }
       MR_GLOBAL T* Rk = R(k);  // constant slots of the Riccati gather plan (frag_plan)
@@ -397,6 +450,119 @@ struct WaveSolver {
     C->in_wd = 0;
     C->wd_short = 0;
     C->wd_trial = 0;
+    C->have_acc = 0;
+    C->tiny = 0;
+    C->delta_it = T(0);
+  }
+
+  // IPOPT's least-square multipliers at the initial point (mr_solver.h Solver::ls_init): the stage QP
+  // min 1/2 sx' M sx + g' sx s.t. the linearised dynamics (c = 0), M = I on the reference's variables +
+  // sum over rows a a^T, g = grad f - sum a rs (rs = v_L - v_U), by the Riccati and forward sweeps; the
+  // costates are the dynamics rows' multipliers, y_d = a.sx - rs; both zero if one exceeds 1000.
+  MR_SWEEP void ls_record() {
+    MR_UNIFORM_P();
+    MR_ASSUME_LDS_STATE();
+    if (own()) {
+      const int k = ln;
+      T z[NZS];
+      load_z(cur, z);
+      MR_GLOBAL T* Rk = R(k);
+      T H[NH], g[NZ];
+      for (int i = 0; i < NH; ++i) H[i] = T(0);
+      for (int i = 0; i < NZ; ++i) g[i] = T(0);
+      if (k < N) {
+        T Hd[36], fx[6], J[48], nz[NX];
+        for (int i = 0; i < NX; ++i) nz[i] = T(0);
+        Dyn<T, MODEL>::fjh(P, z, z + NX, nz, fx, J, Hd);
+        for (int i = 0; i < 48; ++i) Rk[RCF::J + i] = J[i];
+      }
+      for (int i = 0; i < NZ; ++i)
+        if (delta_var(i)) H[hidx(i, i)] = T(1);
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      stage_cost(P, I, k, z, e, sc, g, (T*)nullptr);
+      T d[NI];
+      int act[NI];
+      row_values(k, z, e, d, act);
+#pragma unroll
+      for (int r = 0; r < NROW; ++r) {
+        if (!act[2 * r]) continue;
+        const T nrow = r < 2 ? T(2) : T(1);
+        const T rs = r < 2 ? S(SSF::LAM + 2 * r) - S(SSF::LAM + 2 * r + 1) : T(0);
+#pragma unroll
+        for (int a = 0; a < RN(r); ++a) {
+          g[RI(r, a)] -= T(RS(a)) * rs;
+#pragma unroll
+          for (int bb = a; bb < RN(r); ++bb) H[hidx(RI(r, a), RI(r, bb))] += nrow * T(RS(a)) * T(RS(bb));
+        }
+      }
+      if (lane_active(P, k)) {
+        const int id3[3] = {0, 1, 6};
+        for (int a = 0; a < 3; ++a)
+          for (int bb = a; bb < 3; ++bb) H[hidx(id3[a], id3[bb])] += e.gC[a] * e.gC[bb];
+      }
+      for (int i = 0; i < NH; ++i) Rk[RCF::H + i] = H[i];
+      for (int i = 0; i < NZ; ++i) { Rk[RCF::G0 + i] = g[i]; Rk[RCF::G1 + i] = T(0); Rk[RCF::GD + i] = T(0); }
+      for (int q = 0; q < NHD; ++q) Rk[RCF::HD + q] = T(0);
+      for (int i = 0; i < NX; ++i) Rk[RCF::C + i] = T(0);
+    }
+    wsync(w);
+  }
+  MR_SWEEP void ls_finish() {
+    MR_UNIFORM_P();
+    MR_ASSUME_LDS_STATE();
+    const T big = T(IP_MULT_INIT_MAX);
+    int ok_l = 1;
+    T yv[NI];
+    for (int j = 0; j < NI; ++j) yv[j] = T(0);
+    if (own()) {
+      const int k = ln;
+      T z[NZS], dz[NZS];
+      load_z(cur, z);
+      for (int i = 0; i < NZS; ++i) dz[i] = S(SSF::DZ + i);
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      T d[NI];
+      int act[NI];
+      row_values(k, z, e, d, act);
+#pragma unroll
+      for (int r = 0; r < NROW; ++r) {
+        if (!act[2 * r]) continue;
+        const T adz = row_c(r, dz);
+        if (r < 2) {
+          yv[2 * r] = adz - S(SSF::LAM + 2 * r);
+          yv[2 * r + 1] = adz + S(SSF::LAM + 2 * r + 1);
+        } else {
+          yv[2 * r] = adz;
+        }
+      }
+      if (lane_active(P, k)) yv[JL] = e.gC[0] * dz[0] + e.gC[1] * dz[1] + e.gC[2] * dz[6];
+      for (int j = 0; j < NI; ++j) ok_l &= mr_abs(yv[j]) <= big ? 1 : 0;
+      for (int i = 0; i < NX; ++i)
+        if (i < 6 || (k == 0 && i == 6)) ok_l &= mr_abs(S(SSF::DNU + i)) <= big ? 1 : 0;
+    }
+    const bool ok = wmin(w, ok_l) != 0;
+    if (own()) {
+      for (int i = 0; i < NX; ++i) {
+        NUd(i) = ok ? (double)S(SSF::DNU + i) : 0.0;
+        S(SSF::DNU + i) = T(0);
+      }
+      for (int j = 0; j < NI; ++j) {
+        S(SSF::Y + j) = ok ? yv[j] : T(0);
+        S(SSF::DY + j) = T(0);
+        S(SSF::DS + j) = T(0);
+        S(SSF::DLAM + j) = T(0);
+      }
+    }
+    wsync(w);
+  }
+  MR_HD void ls_init() {
+    cw()->delta_it = T(0);
+    ls_record();
+    if (!riccati<false>(T(0), T(0))) return;
+    T ap, ad, gphi;
+    forward(ap, ad, gphi);
+    ls_finish();
   }
 
   // ---------------- sweep 1: evaluation, KKT error terms, stage QP data (lane = stage) ----------------
@@ -416,8 +582,8 @@ struct WaveSolver {
     auto clip = [&](T v, T x) { return mr_min(mr_max(v, mu_prev / (kappa_sigma * x)), kappa_sigma * mu_prev / x); };
     const int k = ln;
     T st_l = T(0), pr_l = T(0), th_l = T(0), smax_l = T(0), smin_l = T(1e30), nu1_l = T(0), lam1_l = T(0),
-      f_l = T(0), lg_l = T(0);
-    int mi_l = 0;
+      f_l = T(0), lg_l = T(0), preq_l = T(0), viol_l = T(0), y1_l = T(0), lin_l = T(0), pro_l = T(0);
+    int mi_l = 0, mrow_l = 0;
     // lazy multiplier update nu_k += alpha_p * dnu_k (stages 1..N), in fp64; T copies weight the
     // dynamics Hessian
     // refk: the optimality error on the reference's NLP (mr_solver.h MR_KKT_RESTATED); nu_0[0..6] = the
@@ -472,6 +638,7 @@ struct WaveSolver {
         c[8] = z[12] - znext[8];
         c[9] = (k == 0 ? z[11] : z[9]) - znext[9];
         c[10] = (k == 0 ? z[12] : z[10]) - znext[10];
+        for (int i = 0; i < NX; ++i) pro_l = mr_max(pro_l, mr_abs(c[i]));
         if constexpr (RESTO) {  // relaxed vehicle rows F - x' - p + n (the S / previous-control rows are definitions)
           for (int i = 0; i < 6; ++i) {
             const T p = Cf(CSF::CP + i), n = Cf(CSF::CN + i);
@@ -496,7 +663,7 @@ struct WaveSolver {
         }
         for (int i = 0; i < NX; ++i) {
           rbe.st(c[i], 0u, Rk + RCF::C + i);
-          pr_l = mr_max(pr_l, mr_abs(c[i]));
+          preq_l = mr_max(preq_l, mr_abs(c[i]));
           th_l += mr_abs(c[i]);
         }
         for (int i = 0; i < 48; ++i) rbe.st(J[i], 0u, Rk + RCF::J + i);
@@ -553,6 +720,20 @@ struct WaveSolver {
         lam1_l += mr_abs(lam);
         lg_l += mr_log(s);
         mi_l += 1;
+        viol_l = mr_max(viol_l, -d[j]);
+        if (oneslot(j)) lin_l += s;
+        if (yslot(j)) pro_l = mr_max(pro_l, mr_abs(rd));
+        if constexpr (!RESTO) {  // an IPOPT row (y-slot): its multiplier y_d, lazily stepped with alpha_p
+          if (yslot(j)) {
+            const T y = S(SSF::Y + j) + alpha_p * S(SSF::DY + j);
+            S(SSF::Y + j) = y;
+            y_j[j] = y;
+            y1_l += mr_abs(y);
+            mrow_l += 1;
+            pr_l = mr_max(pr_l, mr_abs(rd));
+            th_l += mr_abs(rd);
+          }
+        }
         if constexpr (RESTO) {  // relaxed row d - s - p + n; its multiplier y is its own variable (IPOPT's y_d)
           const T p = Cf(CSF::RP + j), n = Cf(CSF::RN + j);
           const T vp = clip(Cf(CSF::RVP + j) + alpha_d * Cf(CSF::RDVP + j), p);
@@ -572,63 +753,114 @@ struct WaveSolver {
           f_l += rho * (p + n);
           st_l = mr_max(st_l, mr_max(mr_abs(rho + y - vp), mr_abs(rho - y - vn)));
           row_cond_r(d[j], s, lam, p, n, vp, vn, rho, sg_j[j], c0_j[j], c1_j[j]);
+          pr_l = mr_max(pr_l, mr_abs(rd));
+          th_l += mr_abs(rd);
         }
-        pr_l = mr_max(pr_l, mr_abs(rd));
-        th_l += mr_abs(rd);
       }
+      T hd[NHD], gd[NZ];  // the slack shift's pattern and its right-hand side (delta_s), regular phase only
 #pragma unroll
-      for (int r = 0; r < NROW; ++r) {
-        if (!act[2 * r]) continue;
-        T sig_sum = T(0), gsc0 = T(0), gsc1 = T(0), lamdiff = T(0);
+      for (int q = 0; q < NHD; ++q) hd[q] = T(0);
 #pragma unroll
-        for (int sd = 0; sd < 2; ++sd) {
-          int j = 2 * r + sd;
-          T sgn = sd == 0 ? T(1) : T(-1);
-          if constexpr (RESTO) {
+      for (int q = 0; q < NZ; ++q) gd[q] = T(0);
+      if constexpr (RESTO) {
+#pragma unroll
+        for (int r = 0; r < NROW; ++r) {
+          if (!act[2 * r]) continue;
+          T sig_sum = T(0), gsc0 = T(0), gsc1 = T(0), lamdiff = T(0);
+#pragma unroll
+          for (int sd = 0; sd < 2; ++sd) {
+            int j = 2 * r + sd;
+            T sgn = sd == 0 ? T(1) : T(-1);
             sig_sum += sg_j[j];
             gsc0 += sgn * c0_j[j];
             gsc1 += sgn * c1_j[j];
             lamdiff += sgn * y_j[j];
-          } else {
-            T sig = lam_j[j] / s_j[j];
-            sig_sum += sig;
-            gsc0 += sgn * sig * (d[j] - s_j[j]);
-            gsc1 += -sgn / s_j[j];
-            lamdiff += sgn * lam_j[j];
+          }
+#pragma unroll
+          for (int a = 0; a < RN(r); ++a) {
+            const T sa = T(RS(a));
+            g0[RI(r, a)] += sa * gsc0;
+            g1[RI(r, a)] += sa * gsc1;
+            st[RI(r, a)] -= lamdiff * sa;
+#pragma unroll
+            for (int bb = a; bb < RN(r); ++bb) H[hidx(RI(r, a), RI(r, bb))] += sig_sum * sa * T(RS(bb));
           }
         }
-#pragma unroll
-        for (int a = 0; a < RN(r); ++a) {
-          const T sa = T(RS(a));
-          g0[RI(r, a)] += sa * gsc0;
-          g1[RI(r, a)] += sa * gsc1;
-          st[RI(r, a)] -= lamdiff * sa;
-#pragma unroll
-          for (int bb = a; bb < RN(r); ++bb) H[hidx(RI(r, a), RI(r, bb))] += sig_sum * sa * T(RS(bb));
+        if (lane_active(P, k)) {
+          const int id3[3] = {0, 1, 6};
+          const T sig0 = sg_j[JL], sig1 = sg_j[JL + 1];
+          const T lamdiff = y_j[JL] - y_j[JL + 1];
+          const T gz0 = c0_j[JL] - c0_j[JL + 1], gz1 = c1_j[JL] - c1_j[JL + 1];
+          int q = 0;
+          for (int a = 0; a < 3; ++a) {
+            g0[id3[a]] += e.gC[a] * gz0;
+            g1[id3[a]] += e.gC[a] * gz1;
+            st[id3[a]] -= lamdiff * e.gC[a];
+            for (int bb = a; bb < 3; ++bb, ++q)
+              H[hidx(id3[a], id3[bb])] += (sig0 + sig1) * e.gC[a] * e.gC[bb] - lamdiff * e.hC[q];
+          }
         }
-      }
-      if (lane_active(P, k)) {
-        // hard lane rows e_C + m >= 0 (slot JL) and m - e_C >= 0 (JL + 1), nonlinear in (X, Y, S)
-        const int id3[3] = {0, 1, 6};
-        T s0 = s_j[JL], s1 = s_j[JL + 1];
-        T sig0 = lam_j[JL] / s0, sig1 = lam_j[JL + 1] / s1;
-        T lamdiff = lam_j[JL] - lam_j[JL + 1];
-        T gz0 = sig0 * (d[JL] - s0) - sig1 * (d[JL + 1] - s1);
-        T gz1 = -T(1) / s0 + T(1) / s1;
-        if constexpr (RESTO) {
-          sig0 = sg_j[JL];
-          sig1 = sg_j[JL + 1];
-          lamdiff = y_j[JL] - y_j[JL + 1];
-          gz0 = c0_j[JL] - c0_j[JL + 1];
-          gz1 = c1_j[JL] - c1_j[JL + 1];
+      } else {
+        // IPOPT's rows condensed into the stage QP (mr_solver.h Solver::eval_sweep): H += Sigma_s a a^T,
+        // g0 += a Sigma_s (d - s), g1 += a (grad_s phi)/mu (+-kappa_d on a one-sided row), the Lagrangian
+        // gradient y a, the slack stationarity -y - v_L + v_U; hd / gd: delta_s's a a^T and a (d - s)
+#pragma unroll
+        for (int r = 0; r < NROW; ++r) {
+          const int j0 = 2 * r, j1 = j0 + 1;
+          if (!act[j0]) continue;
+          T hs, gr0, gr1, ys, hdw, gdw;
+          if (r < 2) {  // two one-sided rows
+            const T sg0 = lam_j[j0] / s_j[j0], sg1 = lam_j[j1] / s_j[j1];
+            hs = sg0 + sg1;
+            gr0 = sg0 * (d[j0] - s_j[j0]) - sg1 * (d[j1] - s_j[j1]);
+            gr1 = (-T(1) / s_j[j0] + T(IP_KAPPA_D)) + (T(1) / s_j[j1] - T(IP_KAPPA_D));
+            ys = y_j[j0] + y_j[j1];
+            hdw = T(2);
+            gdw = (d[j0] - s_j[j0]) - (d[j1] - s_j[j1]);
+            st_l = mr_max(st_l, mr_max(mr_abs(-y_j[j0] - lam_j[j0]), mr_abs(-y_j[j1] + lam_j[j1])));
+          } else {  // one two-sided row
+            hs = lam_j[j0] / s_j[j0] + lam_j[j1] / s_j[j1];
+            gr0 = hs * (d[j0] - s_j[j0]);
+            gr1 = -T(1) / s_j[j0] + T(1) / s_j[j1];
+            ys = y_j[j0];
+            hdw = T(1);
+            gdw = d[j0] - s_j[j0];
+            st_l = mr_max(st_l, mr_abs(-y_j[j0] - lam_j[j0] + lam_j[j1]));
+          }
+#pragma unroll
+          for (int a = 0; a < RN(r); ++a) {
+            const T sa = T(RS(a));
+            g0[RI(r, a)] += sa * gr0;
+            g1[RI(r, a)] += sa * gr1;
+            st[RI(r, a)] += ys * sa;
+            gd[RI(r, a)] += sa * gdw;
+#pragma unroll
+            for (int bb = 0; bb < RN(r); ++bb) {
+              const int ia = RI(r, a), ib = RI(r, bb);
+              if (ia <= ib) {
+                H[hidx(ia, ib)] += hs * sa * T(RS(bb));
+                hd[hd_slot(ia, ib)] += hdw * sa * T(RS(bb));
+              }
+            }
+          }
         }
-        int q = 0;
-        for (int a = 0; a < 3; ++a) {
-          g0[id3[a]] += e.gC[a] * gz0;
-          g1[id3[a]] += e.gC[a] * gz1;
-          st[id3[a]] -= lamdiff * e.gC[a];
-          for (int bb = a; bb < 3; ++bb, ++q)
-            H[hidx(id3[a], id3[bb])] += (sig0 + sig1) * e.gC[a] * e.gC[bb] - lamdiff * e.hC[q];
+        if (lane_active(P, k)) {  // the lane row: two-sided, nonlinear in (X, Y, S)
+          const int id3[3] = {0, 1, 6};
+          const T hs = lam_j[JL] / s_j[JL] + lam_j[JL + 1] / s_j[JL + 1];
+          const T gr0 = hs * (d[JL] - s_j[JL]), gr1 = -T(1) / s_j[JL] + T(1) / s_j[JL + 1];
+          const T ys = y_j[JL];
+          st_l = mr_max(st_l, mr_abs(-ys - lam_j[JL] + lam_j[JL + 1]));
+          int q = 0;
+          for (int a = 0; a < 3; ++a) {
+            g0[id3[a]] += e.gC[a] * gr0;
+            g1[id3[a]] += e.gC[a] * gr1;
+            st[id3[a]] += ys * e.gC[a];
+            gd[id3[a]] += e.gC[a] * (d[JL] - s_j[JL]);
+            for (int bb = a; bb < 3; ++bb, ++q) {
+              H[hidx(id3[a], id3[bb])] += hs * e.gC[a] * e.gC[bb] + ys * e.hC[q];
+              hd[hd_slot(id3[a], id3[bb])] += e.gC[a] * e.gC[bb];
+            }
+          }
         }
       }
       if constexpr (refk) {  // the reference's variables: X_k here, S_k and U_k with their copies below
@@ -649,7 +881,9 @@ struct WaveSolver {
       for (int i = 0; i < NZ; ++i) {
         rbe.st(T((double)g0[i] + dd[i]), 0u, Rk + RCF::G0 + i);
         rbe.st(g1[i], 0u, Rk + RCF::G1 + i);
+        rbe.st(gd[i], 0u, Rk + RCF::GD + i);
       }
+      for (int q = 0; q < NHD; ++q) rbe.st(hd[q], 0u, Rk + RCF::HD + q);
     }
     if constexpr (refk) {
       // S_k = S_k + Delta-S_{k-1} - Delta-S_k; U_k = u_k + p_{k+1} (U_0: + every w_j); lanes > N hold zeros
@@ -667,7 +901,19 @@ struct WaveSolver {
     const unsigned long long te1 = trace ? MR_CLOCK() : 0ull;
 #endif
     stat_max = wmax(w, st_l);
-    pr_max = wmax(w, pr_l);
+    {
+      auto* C = cw();
+      const T preq = wmax(w, preq_l);
+      pr_max = mr_max(preq, wmax(w, pr_l));
+      const T vio = wmax(w, viol_l), y1v = wsum(w, y1_l), lin = wsum(w, lin_l), pro = wmax(w, pro_l);
+      const int mrw = wsum(w, mrow_l);
+      C->pr_eq = preq;
+      C->viol = vio;
+      C->y1 = y1v;
+      C->lins = lin;
+      C->pr_o = pro;
+      C->mrow = mrw;
+    }
     theta = wsum(w, th_l);
     slam_max = wmax(w, smax_l);
     slam_min = wmin(w, smin_l);
@@ -683,13 +929,30 @@ struct WaveSolver {
 #endif
   }
 
-  MR_HD T kkt_error(T m) const {
-    const T smax = T(100);
-    T sd = mr_max(smax, (nu1 + lam1) / T(me + (mi > 0 ? mi : 1))) / smax;
-    T scm = mr_max(smax, lam1 / T(mi > 0 ? mi : 1)) / smax;
-    T cerr = mr_max(mr_abs(slam_max - m), mr_abs(m - slam_min));
-    if (mi == 0) cerr = T(0);
-    return mr_max(mr_max(stat_max / sd, pr_max), cerr / scm);
+  // IPOPT's error measures (mr_solver.h Solver: s_d, s_c, nlp_error, barrier_error, converged, acceptable)
+  MR_HD T s_d() { return mr_max(T(100), (nu1 + cw()->y1 + lam1) / T(me + cw()->mrow + (mi > 0 ? mi : 1))) / T(100); }
+  MR_HD T s_c() const { return mr_max(T(100), lam1 / T(mi > 0 ? mi : 1)) / T(100); }
+  MR_HD T compl_err(T m) const {
+    if (mi == 0) return T(0);
+    return mr_max(mr_abs(slam_max - m), mr_abs(m - slam_min));
+  }
+  MR_HD T nlp_error(bool rs) {
+    const T pr = rs ? pr_max : mr_max(cw()->pr_eq, cw()->viol);
+    return mr_max(mr_max(stat_max / s_d(), pr), compl_err(T(0)) / s_c());
+  }
+  MR_HD T barrier_error(T m) { return mr_max(mr_max(stat_max / s_d(), pr_max), compl_err(m) / s_c()); }
+  MR_HD T kkt_error(T m) { return barrier_error(m); }
+  MR_HD bool converged(T err) {
+    MR_UNIFORM_P();
+    if (!(err <= P.tol)) return false;
+    return stat_max / sc <= T(IP_DUAL_INF_TOL) && mr_max(cw()->pr_eq, cw()->viol) <= T(IP_CONSTR_VIOL_TOL) &&
+           compl_err(T(0)) / sc <= T(IP_COMPL_INF_TOL);
+  }
+  MR_HD bool acceptable(T err) {
+    MR_UNIFORM_P();
+    if (!(err <= P.acc_tol)) return false;
+    return stat_max / sc <= T(IP_ACC_DUAL_INF) && mr_max(cw()->pr_eq, cw()->viol) <= T(IP_ACC_CONSTR_VIOL) &&
+           compl_err(T(0)) / sc <= T(IP_ACC_COMPL);
   }
 
   // D-register row map of the 16x16x4 MFMA (mr_wave_prims.h) and its inverse
@@ -720,9 +983,10 @@ struct WaveSolver {
   // the lane only (k == 0 differs in two constants) and is built once per factorisation;
   // frag_load issues the 8 gathers unconditionally two stages ahead, frag_finish applies the
   // selects when the stage is factorised, so no load is sunk into a lane-divergent branch.
-  static constexpr int NGATHER = 8;
+  static constexpr int NGATHER = 12;
   struct FragPlan {
-    int off[NGATHER];  // record offsets: data entries, or the record's constant slots (CONE, CZERO, SELP, SEL0)
+    int off[NGATHER];  // record offsets: data entries, or the record's constant slots (CONE, CZERO, SELP, SEL0);
+                       // 8..11: the slack shift's entry of each D register (delta_s: HD, or GD in column 14)
     unsigned dlt;  // D registers on the diagonal of H (+ delta)
     int st_p[4], lp[4];  // per D register: record / LDS targets (discard slots if none)
   };
@@ -751,6 +1015,11 @@ struct WaveSolver {
       const int a_ = a < NZ ? a : 0;
       fp.off[4 + v] = a < NZ ? (c < NZ ? RCF::H + hidx(a_, c) : (c == 14 ? RCF::G0 + a_ : RCF::G1 + a_)) : RCF::CZERO;
       if (a < NZ && a == c && delta_var(a)) fp.dlt |= 1u << v;
+      {
+        const int lo_ = a < c ? a : c, hi_ = a < c ? c : a;
+        const int hs = (a < NZ && c < NZ) ? hd_slot(lo_, hi_) : -1;
+        fp.off[8 + v] = hs >= 0 ? RCF::HD + hs : ((a < NZ && c == 14) ? RCF::GD + a_ : RCF::CZERO);
+      }
       // outputs of D register v: packed-upper P | p (column 14) to the record; the whole tile of P^
       // (both triangles as the product computes them, one LDS write per register) to LDS
       const int junk_r = RCF::JUNK, junk_l = LJUNK_OFF - LP_OFF + lane;  // lp index from LP
@@ -764,12 +1033,14 @@ struct WaveSolver {
 #pragma unroll
     for (int q = 0; q < NGATHER; ++q) raw[q] = rb.ld(ro, (unsigned)fp.off[q]);
   }
-  // operands straight from the gathered words (constants come from the record's constant slots)
-  static MR_HD void frag_finish(const T* dd, const T* raw, T* eb, T* hc) {
+  // operands straight from the gathered words (constants come from the record's constant slots); the
+  // inertia correction: delta on the reference's variables (dd) and delta_s = delta on the slacks (delta x
+  // the gathered slack-shift entry)
+  static MR_HD void frag_finish(const T* dd, T delta, const T* raw, T* eb, T* hc) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) eb[s] = raw[s];
 #pragma unroll
-    for (int v = 0; v < 4; ++v) hc[v] = raw[4 + v] + dd[v];
+    for (int v = 0; v < 4; ++v) hc[v] = raw[4 + v] + dd[v] + delta * raw[8 + v];
   }
 
   // ---------------- sweep 2: Riccati factorisation on the matrix cores ----------------
@@ -863,13 +1134,17 @@ struct WaveSolver {
       const unsigned Rn = R(N);
       const bool row = l < NX;
       const int lr = row ? l : 0, jl = RCF::JUNK, jd = LJUNK_OFF - LP_OFF + l;
-      T hv[NX];  // all loads ahead of the stores (the compiler cannot disambiguate H from P)
-#pragma unroll
-      for (int j = 0; j < NX; ++j) hv[j] = rb.ld(Rn, RCF::H + hidx(lr, j));
-      const T p0 = rb.ld(Rn, RCF::G0 + lr), p1 = rb.ld(Rn, RCF::G1 + lr);
+      T hv[NX], hdv[NX];  // all loads ahead of the stores (the compiler cannot disambiguate H from P)
 #pragma unroll
       for (int j = 0; j < NX; ++j) {
-        const T v = hv[j] + (l == j && delta_var(j) ? delta : T(0));
+        hv[j] = rb.ld(Rn, RCF::H + hidx(lr, j));
+        const int hs = hd_slot(lr < j ? lr : j, lr < j ? j : lr);
+        hdv[j] = rb.ld(Rn, hs >= 0 ? RCF::HD + hs : RCF::CZERO);
+      }
+      const T p0 = rb.ld(Rn, RCF::G0 + lr) + delta * rb.ld(Rn, RCF::GD + lr), p1 = rb.ld(Rn, RCF::G1 + lr);
+#pragma unroll
+      for (int j = 0; j < NX; ++j) {
+        const T v = hv[j] + delta * hdv[j] + (l == j && delta_var(j) ? delta : T(0));
         LP[row ? l * LDS_LD + j : jd] = v;
         rb.st(v, Rn, (row && j >= l) ? RCF::P + pidx(lr, j) : jl);
       }
@@ -886,7 +1161,7 @@ struct WaveSolver {
       // stage offsets as visibly wave-uniform values (SGPR soffsets, not per-lane waterfall loops)
       const unsigned Rk = (unsigned)wu(w, (int)R(k));
       T eb[4], dq[4];
-      frag_finish(dd, raw_use, eb, dq);
+      frag_finish(dd, delta, raw_use, eb, dq);
 #pragma unroll
       for (int v = 0; v < 4; ++v) dq[v] = (dq[v] + s14 * wrow_next(w, dq[v])) * k15;  // g0 + mu g1 | 0
       frag_load(rb, (unsigned)wu(w, (int)R(k >= MR_RIC_AHEAD ? k - MR_RIC_AHEAD : 0)), fp, raw_fill);  // unconditional: k < AHEAD re-read stage 0's record
@@ -917,6 +1192,10 @@ struct WaveSolver {
       T Rh[6] = {qat(11, 11), qat(11, 12), qat(11, 13), qat(12, 12), qat(12, 13), qat(13, 13)};
       T L[6], iv[3];
       const bool piv_ok = chol3r(Rh, L, iv);  // checked every second stage (below)
+      {  // Q_uu's factor for second-order corrections: lanes 0..5 store L10, L20, L21, 1/L00, 1/L11, 1/L22
+        const T lq = l == 0 ? L[1] : (l == 1 ? L[3] : (l == 2 ? L[4] : (l == 3 ? iv[0] : (l == 4 ? iv[1] : iv[2]))));
+        rb.st(lq, Rk, l < 6 ? (unsigned)(RCF::LQ + l) : (unsigned)RCF::JUNK);
+      }
       T w0[3] = {qat(11, 14), qat(12, 14), qat(13, 14)};
       lsolve3r(L, iv, w0);
       T wc[3] = {wshfl(w, dq[dreg(11)], dgrp(11) * 16 + c), wshfl(w, dq[dreg(12)], dgrp(12) * 16 + c),
@@ -1129,17 +1408,7 @@ struct WaveSolver {
         adz[JL + 1] = -gdz;
       }
       for (int i = 0; i < NZS; ++i) S(SSF::DZ + i) = dz[i];
-      for (int j = 0; j < NI; ++j) {
-        if (!act[j]) continue;
-        T s = S(sf(cur) + j), lam = S(SSF::LAM + j);
-        T ds = adz[j] + (d[j] - s);
-        T dl = mu / s - lam - (lam / s) * ds;
-        S(SSF::DS + j) = ds;
-        S(SSF::DLAM + j) = dl;
-        g_l -= mu * ds / s;
-        if (ds < T(0)) ap_l = mr_min(ap_l, -tau * s / ds);
-        if (dl < T(0)) ad_l = mr_min(ad_l, -tau * lam / dl);
-      }
+      row_steps<false>(d, act, adz, tau, ap_l, ad_l, g_l);
     }
     ap = wmin(w, ap_l);
     ad = wmin(w, ad_l);
@@ -1147,6 +1416,56 @@ struct WaveSolver {
 #if MR_PHASE_CYCLES
     if (trace) { tsub[0] += tf1 - tf0; tsub[1] += MR_CLOCK() - tf1; }
 #endif
+  }
+
+  // IPOPT's row steps of this lane's stage (mr_solver.h Solver::forward): the slack step of each row
+  // ds = a.dz + (d - s) (SOC: + the correction's r_soc instead of d - s), the distance steps (a two-sided
+  // row's upper distance: -ds), bound-dual steps dv = mu/t - v - (v/t) dt, the multiplier step
+  // dy = (Sigma_s + delta) ds + grad_s phi - y; into the regular fields or the SOC's (SOC)
+  template <bool SOC>
+  MR_HD void row_steps(const T* d, const int* act, const T* adz, T tau, T& ap_l, T& ad_l, T& g_l) {
+    const T mu = this->mu, dl = cw()->delta_it, kd = T(IP_KAPPA_D);
+#pragma unroll
+    for (int r = 0; r <= NROW; ++r) {
+      const int j0 = r < NROW ? 2 * r : JL, j1 = j0 + 1;
+      if (!act[j0]) continue;
+      const T t0 = S(sf(cur) + j0), t1 = S(sf(cur) + j1);
+      const T l0 = S(SSF::LAM + j0), l1 = S(SSF::LAM + j1);
+      const T s0 = l0 / t0, s1 = l1 / t1;
+      T dt0, dt1, dy0, dy1;
+      if (r < 2) {
+        const T R0 = SOC ? Cf(CSF::SR + j0) : d[j0] - t0;
+        const T R1 = SOC ? Cf(CSF::SR + j1) : -(d[j1] - t1);
+        const T Ds0 = adz[j0] + R0, Ds1 = -adz[j1] + R1;
+        dt0 = Ds0;
+        dt1 = -Ds1;
+        dy0 = (s0 + dl) * Ds0 - mu / t0 + kd * mu - S(SSF::Y + j0);
+        dy1 = (s1 + dl) * Ds1 + mu / t1 - kd * mu - S(SSF::Y + j1);
+        if (!SOC) g_l += kd * mu * (dt0 + dt1);
+      } else {
+        const T R0 = SOC ? Cf(CSF::SR + j0) : d[j0] - t0;
+        const T Ds = adz[j0] + R0;
+        dt0 = Ds;
+        dt1 = -Ds;
+        dy0 = (s0 + s1 + dl) * Ds - mu / t0 + mu / t1 - S(SSF::Y + j0);
+        dy1 = T(0);
+      }
+      const T dv0 = mu / t0 - l0 - s0 * dt0, dv1 = mu / t1 - l1 - s1 * dt1;
+      if constexpr (SOC) {
+        Cf(CSF::SDS + j0) = dt0; Cf(CSF::SDS + j1) = dt1;
+        Cf(CSF::SDLAM + j0) = dv0; Cf(CSF::SDLAM + j1) = dv1;
+        Cf(CSF::SDY + j0) = dy0; Cf(CSF::SDY + j1) = dy1;
+      } else {
+        S(SSF::DS + j0) = dt0; S(SSF::DS + j1) = dt1;
+        S(SSF::DLAM + j0) = dv0; S(SSF::DLAM + j1) = dv1;
+        S(SSF::DY + j0) = dy0; S(SSF::DY + j1) = dy1;
+        g_l -= mu * dt0 / t0 + mu * dt1 / t1;
+      }
+      if (dt0 < T(0)) ap_l = mr_min(ap_l, -tau * t0 / dt0);
+      if (dt1 < T(0)) ap_l = mr_min(ap_l, -tau * t1 / dt1);
+      if (dv0 < T(0)) ad_l = mr_min(ad_l, -tau * l0 / dv0);
+      if (dv1 < T(0)) ad_l = mr_min(ad_l, -tau * l1 / dv1);
+    }
   }
 
   // ---------------- sweep 3 of the restoration phase ----------------
@@ -1278,32 +1597,35 @@ struct WaveSolver {
     wsync(w);  // costate steps of every lane written
   }
 
-  // ---------------- sweep 4: the filter line search (IPOPT backtracking, one SOC) ----------------
-  // The lane's stage iterate, step, slacks and slack steps are loaded once; every trial point is
-  // formed and measured in registers (one pass per trial: the trial's stage values, its dynamics
-  // defect against the neighbour's trial state, three wave sums), and only the accepted point --
-  // or the fallback point when none is acceptable -- is written to iterate buffer 1-cur.
-  // Backtracking (same rules and order as IPOPT's filter line search, Waechter & Biegler 2006):
-  // alpha = ap, ap/2, ... down to a_min; a second-order correction only after the first trial
-  // (nls = 0) when it did not decrease theta; acceptance = theta_max, then the switching /
-  // Armijo or sufficient-decrease test, then the filter.
-  // a0: the first trial step (ap, or ap/2 when the watchdog backtracks from its stored point, nls0 = 1:
-  // the full step was tried); ap: the fraction-to-boundary step (the fallback point's upper clamp)
-  // RESTO: the restoration phase's line search (mr_solver.h trial() with resto set): the relaxations
-  // p, n of the rows and of the vehicle dynamics rows move with the step; theta and phi of the
-  // restoration NLP decide, the point's original theta / barrier objective go to the WaveCold state
-  // (the restoration exit test); no second-order correction.
-  template <bool RESTO>
-  MR_SWEEP void line_search(T th, T ph, T gphi, T a0, T ap, T a_min, T th_pow, int nls0) {
+  // ---------------- sweep 4: the filter line search (IPOPT's backtracking) ----------------
+  // The lane's stage iterate, step, slacks and slack steps are loaded once; every trial point is formed
+  // and measured in registers (one pass per trial: the trial's stage values, its dynamics defect against
+  // the neighbour's trial state, three wave sums), and only the accepted (or forced) point is written to
+  // iterate buffer 1-cur.  Rules (IPOPT's BacktrackingLineSearch / FilterLSAcceptor, mr_solver.h
+  // Solver::backtrack): alpha = a0, a0/2, ... while alpha > a_min (the first trial always); acceptance =
+  // theta_max, then (f-type at the test step size with theta_ref <= theta_min) Armijo or sufficient
+  // decrease (Compare_le, obj_max_inc), then the filter.  Modes (flags):
+  //   LS_WD     watchdog: one trial, judged at the watchdog's step size wd_atest;
+  //   LS_FORCE  one trial, stored whatever its acceptance (the watchdog's tentative full step);
+  //   LS_ACC    one trial, accumulate its constraint values into the SOC right-hand sides
+  //             (SC = acc SC + c(trial), SR = acc SR + (d - s)(trial)), nothing stored;
+  //   otherwise backtracking; a rejected first trial (a0 = the fraction-to-boundary step, theta not
+  //   decreased) returns with LS_NEED_SOC so the caller runs the second-order corrections.
+  // SOCDIR: the trial points lie along the SOC direction (SDZ, SDS) instead of the Newton direction.
+  // RESTO: the restoration phase's NLP (mr_solver.h trial() with resto set).
+  enum { LS_WD = 1, LS_FORCE = 2, LS_ACC = 4, LS_NOSOC = 8 };
+  enum { LSR_ACC = 1, LSR_AUG = 2, LSR_REJF = 4, LSR_NEED_SOC = 8, LSR_FIN = 16 };
+  template <bool RESTO, bool SOCDIR>
+  MR_SWEEP void line_search(T th, T ph, T gphi, T th_pow, T a0, T a_max, T a_min, int nls0, int mode, T a_fix,
+                            T acc) {
     MR_UNIFORM_P();
     MR_ASSUME_LDS_STATE();
-    const T s_phi = T(2.3), delta_sw = T(1), eta = T(1e-4), g_th = T(1e-5), g_ph = T(1e-5);
     const int nb = 1 - cur;
     const int k = ln;
-    const int N = wu(w, this->N);  // wave-uniform: the SOC re-roll's lane index must be an SGPR
+    const int N = wu(w, this->N);
     T z[NZS], dz[NZS], s_c[NI], ds[NI];
     load_z(cur, z);
-    for (int i = 0; i < NZS; ++i) dz[i] = own() ? S(SSF::DZ + i) : T(0);
+    for (int i = 0; i < NZS; ++i) dz[i] = own() ? (SOCDIR ? Cf(CSF::SDZ + i) : S(SSF::DZ + i)) : T(0);
     unsigned actm = 0u;  // active rows of this stage (depend on the stage only, not on the point)
 #pragma unroll
     for (int r = 0; r < NROW; ++r) {
@@ -1316,7 +1638,7 @@ struct WaveSolver {
     for (int j = 0; j < NI; ++j) {
       const bool a = (actm >> j) & 1u;
       s_c[j] = a ? S(sf(cur) + j) : T(1);
-      ds[j] = a ? S(SSF::DS + j) : T(0);
+      ds[j] = a ? (SOCDIR ? Cf(CSF::SDS + j) : S(SSF::DS + j)) : T(0);
     }
     // restoration: the relaxations and their steps (rows of this stage; vehicle rows of x_{k+1})
     T rp[NI], rn[NI], rdp[NI], rdn[NI], cp[6], cn[6], cdp[6], cdn[6], zr[NZS];
@@ -1342,67 +1664,42 @@ struct WaveSolver {
       for (int i = 0; i < NZS; ++i) zr[i] = own() ? Cf(CSF::RZ + i) : T(0);
     }
     T zt[NZS], st[NI];
+    const T kdm = T(IP_KAPPA_D) * mu;
     // one trial point: zt, st (registers), theta, phi; false if a slack is not positive or a value is
-    // not finite
-    auto eval = [&](T alpha, bool soc, T& th_t, T& ph_t) -> bool {
+    // not finite.  accum: add its constraint values to the SOC right-hand sides (SC, SR)
+    auto eval = [&](T alpha, bool accum, T& th_t, T& ph_t) -> bool {
       for (int i = 0; i < NZS; ++i) zt[i] = z[i] + alpha * dz[i];
       if (k == 0)
         for (int i = 0; i < NX; ++i) zt[i] = z[i];  // x_0 fixed
       if (k >= N) { zt[11] = zt[12] = zt[13] = T(0); }
-      T zpl[NZS];
-      for (int i = 0; i < NZS; ++i) zpl[i] = zt[i];
-      if (soc) {
-        // second-order correction: re-roll the shooting states through the dynamics (sequential)
-        T xr[NX], myx[NX];
-        for (int i = 0; i < NX; ++i) { xr[i] = wbcast(w, z[i], 0); myx[i] = xr[i]; }
-        for (int kk = 0; kk < N; ++kk) {
-          T zz[NZS];
-          for (int i = 0; i < NX; ++i) zz[i] = xr[i];
-          zz[11] = wbcast(w, zpl[11], kk);
-          zz[12] = wbcast(w, zpl[12], kk);
-          zz[13] = wbcast(w, zpl[13], kk);
-          zz[14] = T(0);
-          T xn[NX];
-          faug<T, MODEL>(P, kk, zz, xn);
-          for (int i = 0; i < NX; ++i) xr[i] = xn[i];
-          if (ln == kk + 1)
-            for (int i = 0; i < NX; ++i) myx[i] = xr[i];
-        }
-        if (k >= 1)
-          for (int i = 0; i < NX; ++i) zt[i] = myx[i];
-      }
       T ztn[NX];
       for (int i = 0; i < NX; ++i) ztn[i] = wnext(w, zt[i]);
-      T th_l = T(0), f_l = T(0), lg_l = T(0), lgr_l = T(0), tho_l = T(0), fo_l = T(0);
+      T th_l = T(0), f_l = T(0), lg_l = T(0), lgr_l = T(0), tho_l = T(0), fo_l = T(0), lin_l = T(0);
       int ok_l = 1;
       if (own()) {
-        Err<T> e, ep;
+        Err<T> e;
         errors(I, zt[0], zt[1], zt[6], e, false);
-        T d[NI], dp[NI];
+        T d[NI];
         int act[NI];
         row_values(k, zt, e, d, act);
-        if (soc) {
-          errors(I, zpl[0], zpl[1], zpl[6], ep, false);
-          int actp[NI];
-          row_values(k, zpl, ep, dp, actp);
-        }
         for (int j = 0; j < NI; ++j) {
           st[j] = s_c[j];
           if (!((actm >> j) & 1u)) continue;
-          T sj = s_c[j] + alpha * ds[j];
-          if (soc) sj += d[j] - dp[j];
+          const T sj = s_c[j] + alpha * ds[j];
           if (!(sj > T(0))) ok_l = 0;
           st[j] = sj;
           lg_l += mr_log(sj > T(0) ? sj : T(1));
+          if (oneslot(j)) lin_l += sj;
           if constexpr (RESTO) {
             const T pt = rp[j] + alpha * rdp[j], nt = rn[j] + alpha * rdn[j];
             if (!(pt > T(0)) || !(nt > T(0))) ok_l = 0;
             th_l += mr_abs(d[j] - sj - pt + nt);
-            tho_l += mr_abs(d[j] - sj);
+            if (yslot(j)) tho_l += mr_abs(d[j] - sj);
             lgr_l += mr_log(pt > T(0) ? pt : T(1)) + mr_log(nt > T(0) ? nt : T(1));
             f_l += rho * (pt + nt);
-          } else {
+          } else if (yslot(j)) {
             th_l += mr_abs(d[j] - sj);
+            if (accum) Cf(CSF::SR + j) = acc * Cf(CSF::SR + j) + T(slot_sign(j)) * (d[j] - sj);
           }
         }
         if constexpr (RESTO) {
@@ -1411,7 +1708,7 @@ struct WaveSolver {
         } else {
           f_l += stage_cost(P, I, k, zt, e, sc, (T*)nullptr, (T*)nullptr);
         }
-        if (k < N && !soc) {
+        if (k < N) {
           T xn[NX];
           faug<T, MODEL>(P, k, zt, xn);
           if constexpr (RESTO) {
@@ -1428,68 +1725,73 @@ struct WaveSolver {
               th_l += mr_abs(r);
             }
           } else {
-            for (int i = 0; i < NX; ++i) th_l += mr_abs(xn[i] - ztn[i]);
+            for (int i = 0; i < NX; ++i) {
+              th_l += mr_abs(xn[i] - ztn[i]);
+              if (accum) Cf(CSF::SC + i) = acc * Cf(CSF::SC + i) + (xn[i] - ztn[i]);
+            }
           }
         }
       }
       th_t = wsum(w, th_l);
-      const T fv = wsum(w, f_l), lg = wsum(w, lg_l);
+      const T fv = wsum(w, f_l), lg = wsum(w, lg_l), lin = wsum(w, lin_l);
       int ok = wmin(w, ok_l);
-      ph_t = fv - mu * lg;
+      ph_t = fv - mu * lg + kdm * lin;
       if constexpr (RESTO) {
-        ph_t = fv - mu * (lg + wsum(w, lgr_l));
+        ph_t = fv - mu * (lg + wsum(w, lgr_l)) + kdm * lin;
         cw()->tho = wsum(w, tho_l);  // the point as the original problem sees it (restoration exit test)
-        cw()->pho = wsum(w, fo_l) - mu_o * lg;
+        cw()->pho = wsum(w, fo_l) - mu_o * lg + T(IP_KAPPA_D) * mu_o * lin;
       }
       if (!(th_t == th_t) || !(ph_t == ph_t)) ok = 0;
       return wuni(w, ok != 0);
     };
-    T alpha = a0;
-    int nls = nls0, pass = 0, ntr = 0, nsoc = 0;
-    bool accepted = false, ftype = false, rej_filter = false;
-    // backtracking ends below a_min, or below 1e-30: a_min is 0 when theta is (and may flush to 0 in
-    // fp32), and halving alpha to 0 would never leave the loop.  No acceptable step: IPOPT would enter
-    // its restoration phase; this solver takes the shortest tried step (never past the
-    // fraction-to-boundary step, so the slacks stay positive) -- the fallback point.
-    bool fallback = !(alpha >= a_min && alpha >= T(1e-30));
-    if (fallback) alpha = mr_min(mr_max(alpha, a_min), ap);
-    for (;;) {
-      const bool soc = pass == 1;
-      T th_t, ph_t;
-      bool ok = eval(alpha, soc, th_t, ph_t);
+    const LSRef<T> ref{th, ph, gphi, th_pow};
+    T alpha = a0, ph_acc = ph, a_test = a0, th_t = T(0), ph_t = T(0);
+    int nls = nls0, ntr = 0;
+    int flags = 0;
+    bool store = false;
+    if (mode & (LS_FORCE | LS_ACC)) {
+      alpha = a_fix;
+      const bool fin = eval(alpha, (mode & LS_ACC) != 0, th_t, ph_t);
       ntr++;
-      nsoc += soc ? 1 : 0;
-      if (fallback) { ftype = false; break; }
-      if (ok) ok = th_t <= theta_max;
-      if (ok) {
-        const bool sw = gphi < T(0) && alpha * mr_exp(s_phi * mr_log(-gphi)) > delta_sw * th_pow;
-        if (th <= theta_min && sw) {
-          ok = ph_t <= ph + eta * alpha * gphi + T(1e-14) * mr_abs(ph);
-          ftype = true;
-        } else {
-          ok = th_t <= (T(1) - g_th) * th || ph_t <= ph - g_ph * th + T(1e-14) * mr_abs(ph);
-          ftype = false;
+      flags |= fin ? LSR_FIN : 0;
+      store = (mode & LS_FORCE) != 0;
+    } else {
+      for (int n = 0; n < IP_LS_MAX; ++n) {
+        if (!(alpha > a_min || n == 0)) break;
+        a_test = (mode & LS_WD) ? a_fix : alpha;
+        const bool fin = eval(alpha, false, th_t, ph_t);
+        ntr++;
+        bool ok = false;
+        if (fin) {
+          ok = th_t <= theta_max;
+          if (ok) {
+            if (a_test > T(0) && is_ftype(a_test, ref) && th <= theta_min) ok = armijo(ph_t, a_test, ref);
+            else ok = acc_to_iterate(th_t, ph_t, ref);
+          }
+          if (ok && !filter_ok(th_t, ph_t)) { ok = false; flags |= LSR_REJF; }
         }
-      }
-      // the filter last (IPOPT's order), so a rejection by the filter itself is known for the reset
-      // heuristic
-      if (ok && !filter_ok(th_t, ph_t)) { ok = false; rej_filter = true; }
-      if (wuni(w, ok)) { accepted = true; break; }
-      if (!RESTO && pass == 0 && nls == 0 && th_t >= th) { pass = 1; continue; }  // second-order correction
-      pass = 0;
-      alpha *= T(0.5);
-      nls++;
-      if (!(alpha >= a_min && alpha >= T(1e-30))) {
-        fallback = true;
-        alpha = mr_min(mr_max(alpha, a_min), ap);
+        if (wuni(w, ok)) {
+          flags |= LSR_ACC | LSR_FIN;
+          if (!(is_ftype(a_test, ref) && armijo(ph_t, a_test, ref))) flags |= LSR_AUG;
+          ph_acc = ph_t;
+          store = true;
+          break;
+        }
+        if (mode & LS_WD) break;
+        if (!RESTO && !(mode & LS_NOSOC) && fin && n == 0 && alpha == a_max && theta <= th_t) {
+          flags |= LSR_NEED_SOC;  // the caller runs the second-order corrections, then resumes at alpha/2
+          break;
+        }
+        alpha *= T(0.5);
+        nls++;
       }
     }
-    if (own()) {  // the chosen point
+    if (store && own()) {  // the chosen point
       for (int j = 0; j < NI; ++j)
         if ((actm >> j) & 1u) S(sf(nb) + j) = st[j];
       for (int i = 0; i < NZS; ++i) S(zf(nb) + i) = zt[i];
       if constexpr (RESTO) {  // the relaxations move in place (their step is applied once, here)
-        if (accepted) {
+        if (flags & LSR_ACC) {
           for (int j = 0; j < NI; ++j)
             if ((actm >> j) & 1u) {
               Cf(CSF::RP + j) = rp[j] + alpha * rdp[j];
@@ -1504,10 +1806,228 @@ struct WaveSolver {
       }
     }
     res_alpha = alpha;
-    res_flags = (accepted ? 1 : 0) | (ftype ? 2 : 0) | (rej_filter ? 4 : 0);
+    res_flags = flags;
     res_nls = nls;
     res_ntr = ntr;
-    res_nsoc = nsoc;
+    res_th = th_t;
+    res_ph = ph_acc;
+    res_atest = a_test;
+  }
+
+  // FilterLSAcceptor's tests (mr_solver.h Solver: Compare_le with 10 eps |ref|, obj_max_inc 5)
+  static MR_HD bool cmp_le(T lhs, T rhs, T bas) { return lhs - rhs <= T(10) * mr_eps<T>() * mr_abs(bas); }
+  static MR_HD bool is_ftype(T a_test, const LSRef<T>& r) {
+    return r.gphi < T(0) && a_test * mr_exp(T(2.3) * mr_log(-r.gphi)) > r.thpow;
+  }
+  static MR_HD bool armijo(T ph_t, T a_test, const LSRef<T>& r) {
+    return cmp_le(ph_t - r.ph, T(1e-4) * a_test * r.gphi, r.ph);
+  }
+  static MR_HD bool acc_to_iterate(T th_t, T ph_t, const LSRef<T>& r) {
+    if (ph_t > r.ph) {
+      const T bas = mr_abs(r.ph) > T(10) ? mr_log(mr_abs(r.ph)) / mr_log(T(10)) : T(1);
+      if (mr_log(ph_t - r.ph) / mr_log(T(10)) > T(IP_OBJ_MAX_INC) + bas) return false;
+    }
+    const T g = T(1e-5);
+    return cmp_le(th_t, (T(1) - g) * r.th, r.th) || cmp_le(ph_t - r.ph, -g * r.th, r.ph);
+  }
+
+  // ---------------- second-order corrections (IPOPT's TrySecondOrderCorrection, linear) ----------------
+  // mr_solver.h Solver::try_soc / soc_backward: the Newton system re-solved on the stored factorisation
+  // with the constraint right-hand sides c_soc (dynamics rows, CSF::SC) and r_soc (the rows' d - s,
+  // CSF::SR), c_soc = alpha c_soc + c(trial) per correction.  Run by few instances for few iterations, so
+  // the sequential parts are wave-uniform (every lane computes the same, the record read with uniform
+  // addresses) -- written for clarity, like forward_resto.
+  // c_soc, r_soc at the current point (lane = stage)
+  MR_SWEEP void soc_prepare() {
+    MR_UNIFORM_P();
+    MR_ASSUME_LDS_STATE();
+    if (own()) {
+      const int k = ln;
+      for (int i = 0; i < NX; ++i) Cf(CSF::SC + i) = k < N ? R(k)[RCF::C + i] : T(0);
+      T z[NZS];
+      load_z(cur, z);
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      T d[NI];
+      int act[NI];
+      row_values(k, z, e, d, act);
+      for (int j = 0; j < NI; ++j)
+        Cf(CSF::SR + j) = (act[j] && yslot(j)) ? T(slot_sign(j)) * (d[j] - S(sf(cur) + j)) : T(0);
+    }
+    wsync(w);
+  }
+  // the SOC's costate vector and feed-forward: stage gradients with the rows' r_soc (lane = stage), then
+  // pc = P_{k+1} c_k + p_{k+1}, r = g_u + B^T pc, k = -Q_uu^-1 r, p_k = g_x + A^T pc + K^T r (wave-uniform)
+  MR_SWEEP void soc_backward() {
+    MR_UNIFORM_P();
+    MR_ASSUME_LDS_STATE();
+    const T mu = this->mu, dl = cw()->delta_it;
+    const int N = wu(w, this->N);
+    if (own()) {
+      const int k = ln;
+      const MR_GLOBAL T* Rk = R(k);
+      T g[NZ];
+      for (int i = 0; i < NZ; ++i) g[i] = Rk[RCF::G0 + i] + mu * Rk[RCF::G1 + i] + dl * Rk[RCF::GD + i];
+      T z[NZS];
+      load_z(cur, z);
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      T d[NI];
+      int act[NI];
+      row_values(k, z, e, d, act);
+#pragma unroll
+      for (int r = 0; r <= NROW; ++r) {
+        const int j0 = r < NROW ? 2 * r : JL, j1 = j0 + 1;
+        if (!act[j0]) continue;
+        const T t0 = S(sf(cur) + j0), t1 = S(sf(cur) + j1);
+        const T s0 = S(SSF::LAM + j0) / t0, s1 = S(SSF::LAM + j1) / t1;
+        T dg;
+        if (r < 2) dg = (s0 + dl) * (Cf(CSF::SR + j0) - (d[j0] - t0)) + (s1 + dl) * (Cf(CSF::SR + j1) + (d[j1] - t1));
+        else dg = (s0 + s1 + dl) * (Cf(CSF::SR + j0) - (d[j0] - t0));
+        if (r < NROW) {
+#pragma unroll
+          for (int a = 0; a < RN(r); ++a) g[RI(r, a)] += T(RS(a)) * dg;
+        } else {
+          g[0] += e.gC[0] * dg;
+          g[1] += e.gC[1] * dg;
+          g[6] += e.gC[2] * dg;
+        }
+      }
+      for (int i = 0; i < NZ; ++i) Cf(CSF::SG + i) = g[i];
+    }
+    wsync(w);
+    const MR_GLOBAL T* cb = rc + (int64_t)RC_STRIDE * WL;
+    T pv[NX];
+    for (int i = 0; i < NX; ++i) pv[i] = cb[(CSF::SG + i) * WL + N];
+    if (ln == N)
+      for (int i = 0; i < NX; ++i) Cf(CSF::SPV + i) = pv[i];
+    for (int k = N - 1; k >= 0; --k) {
+      const MR_GLOBAL T* Rk = R(k);
+      const MR_GLOBAL T* Rn = R(k + 1);
+      T J[48];
+      for (int i = 0; i < 48; ++i) J[i] = Rk[RCF::J + i];
+      T pc[NX];
+      for (int i = 0; i < NX; ++i) {
+        T acc = pv[i];
+        for (int l = 0; l < NX; ++l) acc += Rn[RCF::P + pidx(i, l)] * cb[(CSF::SC + l) * WL + k];
+        pc[i] = acc;
+      }
+      T r[NU];
+      apply_Bt(J, k, pc, r);
+      for (int a = 0; a < NU; ++a) r[a] += cb[(CSF::SG + NX + a) * WL + k];
+      // k = -Q_uu^-1 r with Q_uu = L L^T (L10, L20, L21, reciprocal pivots from the Riccati sweep)
+      const T L1 = Rk[RCF::LQ + 0], L3 = Rk[RCF::LQ + 1], L4 = Rk[RCF::LQ + 2];
+      const T iv[3] = {Rk[RCF::LQ + 3], Rk[RCF::LQ + 4], Rk[RCF::LQ + 5]};
+      const T Lf[6] = {T(0), L1, T(0), L3, L4, T(0)};
+      T kf[NU] = {-r[0], -r[1], -r[2]};
+      lsolve3r(Lf, iv, kf);
+      ltsolve3r(Lf, iv, kf);
+      T at[NX];
+      apply_At(J, k, pc, at);
+      for (int i = 0; i < NX; ++i) {
+        T v = cb[(CSF::SG + i) * WL + k] + at[i];
+        for (int a = 0; a < NU; ++a) v += Rk[RCF::K + a * NX + i] * r[a];
+        pv[i] = v;
+      }
+      if (ln == k) {
+        for (int a = 0; a < NU; ++a) Cf(CSF::SK0 + a) = kf[a];
+        for (int i = 0; i < NX; ++i) Cf(CSF::SPV + i) = pv[i];
+      }
+    }
+    wsync(w);
+  }
+  // the SOC direction (mr_solver.h Solver::forward with soc set): SDZ, SDS, SDLAM, SDY, SDNU
+  MR_SWEEP void forward_soc(T& ap, T& ad) {
+    MR_UNIFORM_P();
+    MR_ASSUME_LDS_STATE();
+    const T tau = mr_max(T(0.99), T(1) - mu);
+    const int N = wu(w, this->N);
+    const MR_GLOBAL T* cb = rc + (int64_t)RC_STRIDE * WL;
+    T dx[NX], mydz[NZS];
+    for (int i = 0; i < NX; ++i) dx[i] = T(0);
+    for (int i = 0; i < NZS; ++i) mydz[i] = T(0);
+    if (ln == 0 && !MR_KKT_RESTATED)  // the initial-state rows' multiplier step: stage 0's costate
+      for (int i = 0; i < NX; ++i) Cf(CSF::SDNU + i) = Cf(CSF::SPV + i);
+    for (int k = 0; k <= N; ++k) {
+      const MR_GLOBAL T* Rk = R(k);
+      T du[NU] = {T(0), T(0), T(0)};
+      if (k < N)
+        for (int a = 0; a < NU; ++a) {
+          T v = cb[(CSF::SK0 + a) * WL + k];
+          for (int j = 0; j < NX; ++j) v += Rk[RCF::K + a * NX + j] * dx[j];
+          du[a] = v;
+        }
+      if (ln == k) {
+        for (int i = 0; i < NX; ++i) mydz[i] = dx[i];
+        for (int a = 0; a < NU; ++a) mydz[NX + a] = du[a];
+      }
+      if (k == N) break;
+      T J[48], t[NX], tb[NX];
+      for (int i = 0; i < 48; ++i) J[i] = Rk[RCF::J + i];
+      apply_A(J, k, dx, t);
+      apply_B(J, k, du, tb);
+      for (int i = 0; i < NX; ++i) dx[i] = t[i] + tb[i] + cb[(CSF::SC + i) * WL + k];
+      if (ln == k + 1) {  // the costate (multiplier) step of x_{k+1}'s rows
+        const MR_GLOBAL T* Rn = R(k + 1);
+        for (int i = 0; i < NX; ++i) {
+          T v = Cf(CSF::SPV + i);
+          for (int l = 0; l < NX; ++l) v += Rn[RCF::P + pidx(i, l)] * dx[l];
+          Cf(CSF::SDNU + i) = v;
+        }
+      }
+    }
+    T ap_l = T(1), ad_l = T(1), g_l = T(0);
+    if (own()) {
+      const int k = ln;
+      T dz[NZS];
+      for (int i = 0; i < NZS; ++i) dz[i] = mydz[i];
+      T z[NZS];
+      load_z(cur, z);
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      T d[NI];
+      int act[NI];
+      row_values(k, z, e, d, act);
+      T adz[NI];
+#pragma unroll
+      for (int r = 0; r < NROW; ++r) {
+        const T v = row_c(r, dz);
+        adz[2 * r] = v;
+        adz[2 * r + 1] = -v;
+      }
+      dz[14] = T(0);
+      adz[JL] = adz[JL + 1] = adz[JL + 2] = T(0);
+      if (lane_active(P, k)) {
+        const T gdz = e.gC[0] * dz[0] + e.gC[1] * dz[1] + e.gC[2] * dz[6];
+        adz[JL] = gdz;
+        adz[JL + 1] = -gdz;
+      }
+      for (int i = 0; i < NZS; ++i) Cf(CSF::SDZ + i) = dz[i];
+      row_steps<true>(d, act, adz, tau, ap_l, ad_l, g_l);
+    }
+    ap = wmin(w, ap_l);
+    ad = wmin(w, ad_l);
+    wsync(w);
+  }
+  // the accepted correction becomes the iteration's direction; returns its dual step size
+  MR_SWEEP T soc_commit() {
+    MR_ASSUME_LDS_STATE();
+    const T tau = mr_max(T(0.99), T(1) - mu);
+    T ad_l = T(1);
+    if (own()) {
+      for (int i = 0; i < NZS; ++i) S(SSF::DZ + i) = Cf(CSF::SDZ + i);
+      for (int j = 0; j < NI; ++j) {
+        const T dl = Cf(CSF::SDLAM + j), lam = S(SSF::LAM + j);
+        S(SSF::DS + j) = Cf(CSF::SDS + j);
+        S(SSF::DLAM + j) = dl;
+        S(SSF::DY + j) = Cf(CSF::SDY + j);
+        if (lam != T(0) && dl < T(0)) ad_l = mr_min(ad_l, -tau * lam / dl);
+      }
+      for (int i = 0; i < NX; ++i) S(SSF::DNU + i) = Cf(CSF::SDNU + i);
+    }
+    const T ad = wmin(w, ad_l);
+    wsync(w);
+    return ad;
   }
 
   MR_HD bool filter_ok(T th, T ph) const {
@@ -1542,6 +2062,7 @@ struct WaveSolver {
       for (int j = 0; j < NI; ++j) {
         Cf(CSF::WSL + j) = S(sf(cur) + j); Cf(CSF::WLAM + j) = S(SSF::LAM + j);
         Cf(CSF::WDS + j) = S(SSF::DS + j); Cf(CSF::WDLAM + j) = S(SSF::DLAM + j);
+        Cf(CSF::WY + j) = S(SSF::Y + j); Cf(CSF::WDY + j) = S(SSF::DY + j);
       }
       for (int i = 0; i < NX; ++i) { WNUd(i) = NUd(i); Cf(CSF::WDNU + i) = S(SSF::DNU + i); }
     }
@@ -1554,6 +2075,7 @@ struct WaveSolver {
       for (int j = 0; j < NI; ++j) {
         S(sf(cur) + j) = Cf(CSF::WSL + j); S(SSF::LAM + j) = Cf(CSF::WLAM + j);
         S(SSF::DS + j) = Cf(CSF::WDS + j); S(SSF::DLAM + j) = Cf(CSF::WDLAM + j);
+        S(SSF::Y + j) = Cf(CSF::WY + j); S(SSF::DY + j) = Cf(CSF::WDY + j);
       }
       for (int i = 0; i < NX; ++i) { NUd(i) = WNUd(i); S(SSF::DNU + i) = Cf(CSF::WDNU + i); }
     }
@@ -1566,7 +2088,7 @@ struct WaveSolver {
     MR_ASSUME_LDS_STATE();
     const T g_th = T(1e-5), g_ph = T(1e-5), rho = T(RESTO_RHO);
     auto* C = cw();
-    filter_add((T(1) - g_th) * th, ph - g_ph * th);
+    filter_add((T(1) - g_th) * th, ph - g_ph * th);  // PrepareRestoPhaseStart: the entry point augments the filter
     C->onfilt = nfilt;
     for (int i = 0; i < 2 * FMAX; ++i) C->ofilt[i] = filt[i];
     C->mu_o = mu;
@@ -1589,11 +2111,14 @@ struct WaveSolver {
       row_values(k, z, e, d, act);
       for (int j = 0; j < NI; ++j) {
         T p = T(1), n = T(1);
+        Cf(CSF::RS0 + j) = S(sf(cur) + j);
+        Cf(CSF::RLAM + j) = S(SSF::LAM + j);
         if (act[j]) {
           const T s = S(sf(cur) + j), c = d[j] - s;
-          th_rows_l += mr_abs(c);
+          if (yslot(j)) th_rows_l += mr_abs(c);
           resto_pn(c, mu_r, rho, p, n);
-          S(SSF::LAM + j) = mu_r / s;  // the slacks' bound duals restart at complementarity with mu_R
+          // the slacks' bound duals: the original problem's, but not above rho (RestoIterateInitializer)
+          S(SSF::LAM + j) = mr_min(S(SSF::LAM + j), rho);
         }
         Cf(CSF::RP + j) = p;
         Cf(CSF::RN + j) = n;
@@ -1638,16 +2163,55 @@ struct WaveSolver {
     return wuni(w, ok);
   }
   MR_SWEEP void resto_exit() {
+    // mr_solver.h Solver::resto_exit: a two-sided row's distances rescaled to one slack; bound duals by a
+    // complementarity Newton step over the whole restoration (dual fraction to the boundary), all reset to 1
+    // if one exceeds 1000; y = 0; the original problem's barrier parameter, filter, perturbation state
+    MR_UNIFORM_P();
     MR_ASSUME_LDS_STATE();
     auto* C = cw();
     const T mu_o = C->mu_o;
+    const T tau = mr_max(T(0.99), T(1) - mu_o);
+    T ad_l = T(1), vmax_l = T(0);
+    if (own()) {
+      const int k = ln;
+      T z[NZS];
+      load_z(cur, z);
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      T d[NI];
+      int act[NI];
+      row_values(k, z, e, d, act);
+      for (int r = 2; r <= NROW; ++r) {
+        const int j0 = r < NROW ? 2 * r : JL;
+        if (!act[j0]) continue;
+        const T t0 = S(sf(cur) + j0), t1 = S(sf(cur) + j0 + 1), rng = d[j0] + d[j0 + 1];
+        S(sf(cur) + j0) = t0 * rng / (t0 + t1);
+        S(sf(cur) + j0 + 1) = t1 * rng / (t0 + t1);
+      }
+      for (int j = 0; j < NI; ++j) {
+        S(SSF::DLAM + j) = T(0);
+        if (!act[j]) continue;
+        const T t0 = Cf(CSF::RS0 + j), v0 = Cf(CSF::RLAM + j), t = S(sf(cur) + j);
+        const T dv = mu_o / t0 - v0 - v0 / t0 * (t - t0);
+        S(SSF::DLAM + j) = dv;
+        if (dv < T(0)) ad_l = mr_min(ad_l, -tau * v0 / dv);
+      }
+    }
+    const T ad = wmin(w, ad_l);
+    if (own())
+      for (int j = 0; j < NI; ++j) {
+        const T v0 = Cf(CSF::RLAM + j);
+        const T v = v0 == T(0) ? T(0) : v0 + ad * S(SSF::DLAM + j);
+        S(SSF::LAM + j) = v;
+        vmax_l = mr_max(vmax_l, mr_abs(v));
+      }
+    const T vmax = wmax(w, vmax_l);
     if (own()) {
       for (int j = 0; j < NI; ++j) {
-        const T s = S(sf(cur) + j), lam0 = S(SSF::LAM + j), lam = lam0 + alpha_d * S(SSF::DLAM + j);
-        T lnew = mu_o / s;
-        if (mr_abs(lnew - lam) > T(RESTO_MULT_RESET)) lnew = T(1);
-        S(SSF::LAM + j) = lam0 == T(0) ? T(0) : lnew;  // inactive slots stay 0
+        if (vmax > T(RESTO_MULT_RESET) && Cf(CSF::RLAM + j) != T(0)) S(SSF::LAM + j) = T(1);
         S(SSF::DLAM + j) = T(0);
+        S(SSF::Y + j) = T(0);
+        S(SSF::DY + j) = T(0);
       }
       for (int i = 0; i < NX; ++i) { NUd(i) = 0.0; S(SSF::DNU + i) = T(0); }
     }
@@ -1661,17 +2225,32 @@ struct WaveSolver {
     C->resto = 0;
     wsync(w);
   }
+  // IPOPT's backup acceptable iterate: stored when the current point is acceptable (primal part: what
+  // the solve returns), returned if the line search later fails at an almost feasible point
+  MR_SWEEP void acc_save() {
+    MR_ASSUME_LDS_STATE();
+    if (own())
+      for (int i = 0; i < NZS; ++i) Cf(CSF::AZ + i) = S(zf(cur) + i);
+    cw()->have_acc = 1;
+    wsync(w);
+  }
+  MR_SWEEP void acc_restore() {
+    MR_ASSUME_LDS_STATE();
+    if (own())
+      for (int i = 0; i < NZS; ++i) S(zf(cur) + i) = Cf(CSF::AZ + i);
+    wsync(w);
+  }
 
-  // ---------------- the IPM loop (wave-uniform control) ----------------
+  // ---------------- the IPM loop (wave-uniform control; mr_solver.h Solver::solve, same rules) ----------------
   MR_HD SolveOut solve() {
     MR_UNIFORM_P();
     const T kappa_eps = T(10), kappa_mu = T(0.2), theta_mu = T(1.5);
-    const T mu_min = P.tol / T(10);
-    const T s_phi = T(2.3), s_theta = T(1.1), delta_sw = T(1), eta = T(1e-4), g_th = T(1e-5), g_ph = T(1e-5);
+    // IPOPT's monotone update keeps mu >= min(tol, compl_inf_tol) / (barrier_tol_factor + 1)
+    const T mu_min = mr_max(T(1e-11), mr_min(P.tol, T(IP_COMPL_INF_TOL)) / (kappa_eps + T(1)));
+    const T g_th = T(1e-5), g_ph = T(1e-5);
     SolveOut out{2, 0, 0.0, 0.0};
     T mu_prev = mu;
     int acc_count = 0;
-    int ls_fail = 0;  // consecutive iterations without an acceptable line-search step
     // IPOPT's filter reset heuristic (filter_reset_trigger = 5, max_filter_resets = 5): after this many
     // successive iterations whose line search had a trial point rejected by the filter, clear it
     int filt_rej_iters = 0, filt_resets = 0;
@@ -1699,36 +2278,40 @@ struct WaveSolver {
       MR_T0();
       if (rs) eval_sweep<true>(mu_prev); else eval_sweep<false>(mu_prev);
       MR_T1(0);
-      T kkt = kkt_error(T(0));
+      const T kkt = nlp_error(rs);
       if (!(kkt == kkt) || !(fval == fval)) { out.status = 3; break; }
       if (rs) {
-        // the restoration NLP converged at a point the original problem does not accept: IPOPT's
-        // "converged to a point of local infeasibility"
-        if (kkt <= P.tol) { out.status = MR_STATUS_INFEASIBLE; break; }
+        // the restoration NLP converged at a point the original problem does not accept: restoration
+        // failed when that point is feasible to 1e2 tol (IPOPT), else a point of local infeasibility
+        if (kkt <= P.tol) { out.status = cw()->pr_o <= T(100) * P.tol ? 3 : MR_STATUS_INFEASIBLE; break; }
       } else {
         out.kkt = (double)kkt;
         out.obj = (double)(fval / sc);
-        if (kkt <= P.tol) { out.status = 0; break; }
+        if (converged(kkt)) { out.status = 0; break; }
         if (P.acc_iter > 0) {
-          acc_count = (kkt <= P.acc_tol) ? acc_count + 1 : 0;
+          acc_count = acceptable(kkt) ? acc_count + 1 : 0;
           if (acc_count >= P.acc_iter) { out.status = 1; break; }
         }
       }
       if (it >= P.max_iter) { out.status = 2; break; }
       T mu_old = mu;
-      while (kkt_error(mu) <= kappa_eps * mu && mu > mu_min) {
-        T m1 = kappa_mu * mu, m2 = mr_exp(theta_mu * mr_log(mu));
-        mu = mr_max(mu_min, mr_min(m1, m2));
+      while (barrier_error(mu) <= kappa_eps * mu) {
+        const T m1 = kappa_mu * mu, m2 = mr_exp(theta_mu * mr_log(mu));
+        const T mn = mr_max(mu_min, mr_min(m1, m2));
+        if (mn == mu) break;
+        mu = mn;
       }
       if (mu != mu_old) {  // IPOPT resets its line search with a new barrier problem: filter and watchdog
         nfilt = 0;
         cw()->in_wd = 0;
         cw()->wd_short = 0;
       }
+      const T ph_cur = fval - mu * logs + T(IP_KAPPA_D) * mu * cw()->lins;  // barrier objective (+ damping)
+      // inertia-corrected factorisation (IPOPT's PDPerturbationHandler, mr_solver.h)
       T delta = T(0);
       bool first = true, fact_ok = false;
       MR_T0();
-      for (int tries = 0; tries < 60; ++tries) {
+      for (int tries = 0; tries < 200; ++tries) {
         MR_CNT(6);
 #if MR_PHASE_CYCLES
         const unsigned long long tr0 = trace ? MR_CLOCK() : 0ull;
@@ -1742,34 +2325,36 @@ struct WaveSolver {
           delta = delta_last == T(0) ? T(1e-4) : mr_max(T(1e-20), delta_last / T(3));
           first = false;
         } else {
-          delta *= (delta_last == T(0) ? T(100) : T(8));
+          delta *= (delta_last == T(0) || T(1e5) * delta_last < delta) ? T(100) : T(8);
         }
         if (delta > T(1e40)) break;
       }
       MR_T1(1);
-      if (!fact_ok) { out.status = 3; break; }
+      if (!fact_ok) {
+        if (rs) { out.status = 3; break; }
+        // IPOPT: no inertia-correct factorisation -> the restoration phase
+        resto_enter(theta, ph_cur);
+        mu_prev = mu;
+        cw()->in_wd = 0;
+        cw()->wd_short = 0;
+        acc_count = 0;
+        continue;
+      }
       if (delta > T(0)) delta_last = delta;
+      cw()->delta_it = delta;
       T &ap = res_ap, &ad = res_ad, &gphi = res_gphi;
       MR_T0();
       if (rs) forward_resto(ap, ad, gphi); else forward(ap, ad, gphi);
       MR_T1(2);
-      T th = theta, ph = fval - mu * logs;
-      T th_pow = mr_exp(s_theta * mr_log(mr_max(th, T(1e-30))));
-      T a_min;
-      if (gphi < T(0)) {
-        T t1 = g_ph * th / (-gphi);
-        T t2 = delta_sw * th_pow / mr_exp(s_phi * mr_log(-gphi));
-        // IPOPT (W&B 2006 eq. 23, CalculateAlphaMin): the switching term only at theta <= theta_min
-        a_min = T(0.05) * mr_min(g_th, th <= theta_min ? mr_min(t1, t2) : t1);
-      } else {
-        a_min = T(0.05) * g_th;
-      }
+      T th = theta, ph = ph_cur;
+      T th_pow = mr_exp(T(1.1) * mr_log(mr_max(th, T(1e-30))));
+      T a_min = alpha_min_of(th, gphi);
       if (rs) {  // a restoration-phase step: its own filter, no watchdog, no second-order correction
         MR_T0();
-        line_search<true>(th, ph, gphi, ap, ap, a_min, th_pow, 0);
+        line_search<true, false>(th, ph, gphi, th_pow, ap, ap, a_min, 0, 0, T(0), T(-1));
         MR_T1(3);
-        if (!(res_flags & 1)) { out.status = 3; break; }  // IPOPT: restoration failed
-        if (!(res_flags & 2)) filter_add((T(1) - g_th) * th, ph - g_ph * th);
+        if (!(res_flags & LSR_ACC)) { out.status = 3; break; }  // IPOPT: restoration failed
+        if (res_flags & LSR_AUG) filter_add((T(1) - g_th) * th, ph - g_ph * th);
         if (trace && ln == 0 && it < trace_cap - 2) {
           double* tr = trace + 8 * it;
           tr[0] = (double)kkt; tr[1] = (double)mu; tr[2] = (double)res_alpha; tr[3] = (double)ad;
@@ -1790,10 +2375,12 @@ struct WaveSolver {
         }
         continue;
       }
+      if (acceptable(kkt)) acc_save();  // IPOPT stores the current iterate if it is acceptable
 #if MR_WD_TRIGGER > 0
       // IPOPT's watchdog (mr_solver.h, same rule): after watchdog_shortened_iter_trigger successive
       // shortened steps store the iterate and direction, take full steps tentatively, judged against the
-      // stored point; after watchdog_trial_iter_max without an acceptable one, back to the stored point
+      // stored point at its step size; after watchdog_trial_iter_max without an acceptable one, back to the
+      // stored point and a regular backtracking line search that skips the full step
       if (!cw()->in_wd && cw()->wd_short >= MR_WD_TRIGGER) {
         wd_save();
         auto* C = cw();
@@ -1803,18 +2390,26 @@ struct WaveSolver {
         C->wd_trial = 0;
       }
 #endif
-      bool take_anyway = false;
+      bool take_anyway = false, accepted = false, soc_taken = false, rejf = false;
+      T alpha = ap;
+      T uth = th, uph = ph;  // the accepting line search's reference (the filter entry on augmentation)
+      int flags = 0;
       MR_T0();
       if (wuni(w, cw()->in_wd != 0)) {
         auto* C = cw();
-        line_search<false>(C->wd_th, C->wd_ph, C->wd_gphi, ap, ap, ap, C->wd_thpow, 0);
-        if (res_flags & 1) {
+        line_search<false, false>(C->wd_th, C->wd_ph, C->wd_gphi, C->wd_thpow, ap, ap, ap, 0, LS_WD, C->wd_ap,
+                                  T(-1));
+        flags = res_flags;
+        rejf |= (flags & LSR_REJF) != 0;
+        uth = C->wd_th;
+        uph = C->wd_ph;
+        if (flags & LSR_ACC) {
+          accepted = true;
           C->in_wd = 0;
           C->wd_short = 0;
-          th = C->wd_th;  // the filter entry is the watchdog point's (the acceptor's reference)
-          ph = C->wd_ph;
         } else if (++C->wd_trial <= MR_WD_TRIAL_MAX) {
-          take_anyway = true;  // the line search stored the plain full step (its fallback point at ap)
+          take_anyway = true;  // the full step is taken tentatively
+          line_search<false, false>(th, ph, gphi, th_pow, ap, ap, ap, 0, LS_FORCE, ap, T(-1));
         } else {
           // back to the watchdog point: its iterate and direction, a regular backtracking line search
           // that skips the full step
@@ -1823,21 +2418,68 @@ struct WaveSolver {
           C->wd_short = 0;
           th = C->wd_th; ph = C->wd_ph; gphi = C->wd_gphi; ap = C->wd_ap; ad = C->wd_ad; a_min = C->wd_amin;
           th_pow = C->wd_thpow;
-          line_search<false>(th, ph, gphi, T(0.5) * ap, ap, a_min, th_pow, 1);
+          line_search<false, false>(th, ph, gphi, th_pow, T(0.5) * ap, ap, a_min, 1, LS_NOSOC, T(0), T(-1));
+          flags = res_flags;
+          rejf |= (flags & LSR_REJF) != 0;
+          accepted = (flags & LSR_ACC) != 0;
         }
       } else {
-        line_search<false>(th, ph, gphi, ap, ap, a_min, th_pow, 0);
+        line_search<false, false>(th, ph, gphi, th_pow, ap, ap, a_min, 0, 0, T(0), T(-1));
+        flags = res_flags;
+        rejf |= (flags & LSR_REJF) != 0;
+        accepted = (flags & LSR_ACC) != 0;
+        if (flags & LSR_NEED_SOC) {
+          // IPOPT's TrySecondOrderCorrection: up to max_soc (4) linear corrections while theta falls by
+          // kappa_soc (0.99); then, if none is accepted, the backtracking resumes at alpha / 2
+          const T a_trial = res_alpha, a_test0 = res_atest;
+          T th_trial = res_th, a_soc = a_trial, th_old = T(0);
+          soc_prepare();
+          for (int count = 0; count < IP_MAX_SOC; ++count) {
+            if (count > 0 && !(th_trial <= T(IP_KAPPA_SOC) * th_old)) break;
+            th_old = th_trial;
+            if (count == 0)
+              line_search<false, false>(th, ph, gphi, th_pow, a_soc, ap, a_min, 0, LS_ACC, a_soc, a_soc);
+            else
+              line_search<false, true>(th, ph, gphi, th_pow, a_soc, ap, a_min, 0, LS_ACC, a_soc, a_soc);
+            soc_backward();
+            T aps, ads;
+            forward_soc(aps, ads);
+            line_search<false, true>(th, ph, gphi, th_pow, aps, aps, aps, 0, LS_WD, a_test0, T(-1));
+            rejf |= (res_flags & LSR_REJF) != 0;
+            a_soc = aps;
+            if (!(res_flags & LSR_FIN)) break;
+            if (res_flags & LSR_ACC) {
+              soc_taken = accepted = true;
+              flags = res_flags;
+              ad = soc_commit();
+              break;
+            }
+            th_trial = res_th;
+          }
+          if (!soc_taken) {
+            line_search<false, false>(th, ph, gphi, th_pow, T(0.5) * a_trial, ap, a_min, 1, LS_NOSOC, T(0), T(-1));
+            flags = res_flags;
+            rejf |= (flags & LSR_REJF) != 0;
+            accepted = (flags & LSR_ACC) != 0;
+          }
+        }
       }
       MR_T1(3);
 #if MR_PHASE_CYCLES
       cyc[4] += res_ntr;
-      cyc[5] += res_nsoc;
+      cyc[5] += soc_taken ? 1 : 0;
 #endif
-      const T alpha = res_alpha;
-      const bool accepted = (res_flags & 1) && !take_anyway, ftype = res_flags & 2, rej_filter = res_flags & 4;
+      alpha = res_alpha;
       const int nls = res_nls;
-      // no acceptable step at an infeasible point: the restoration phase (from the next iteration on)
-      if (!accepted && !take_anyway && pr_max > P.tol) {
+      if (!accepted && !take_anyway) {
+        // IPOPT on a failed line search (the soft restoration phase is not restated): the
+        // current point acceptable -> "acceptable point reached"; almost feasible (theta <= 1e-2 tol) ->
+        // the stored acceptable point or restoration failed; otherwise the restoration phase
+        if (acceptable(kkt)) { out.status = 1; break; }
+        if (theta <= T(1e-2) * P.tol) {
+          if (cw()->have_acc) { acc_restore(); out.status = 1; } else { out.status = 3; }
+          break;
+        }
         resto_enter(th, ph);
         mu_prev = mu;
         cw()->in_wd = 0;
@@ -1850,14 +2492,10 @@ struct WaveSolver {
         }
         continue;
       }
-      // no acceptable step at a point feasible to the tolerance: the shortest tried step (the line
-      // search's fallback point); after MR_LS_FAIL_MAX such iterations in a row the solve stops
-      ls_fail = (accepted || take_anyway) ? 0 : ls_fail + 1;
-      if (ls_fail >= MR_LS_FAIL_MAX) { out.status = 3; break; }
       if (!take_anyway) cw()->wd_short = (accepted && alpha < ap) ? cw()->wd_short + 1 : 0;
 #if MR_FILTER_RESET_TRIGGER > 0
       if (filt_resets < MR_MAX_FILTER_RESETS) {
-        filt_rej_iters = rej_filter ? filt_rej_iters + 1 : 0;
+        filt_rej_iters = rejf ? filt_rej_iters + 1 : 0;
         if (filt_rej_iters >= MR_FILTER_RESET_TRIGGER) {
           nfilt = 0;
           filt_resets++;
@@ -1865,12 +2503,13 @@ struct WaveSolver {
         }
       }
 #endif
-      if (!(ftype && accepted) && !take_anyway) filter_add((T(1) - g_th) * th, ph - g_ph * th);
+      // IPOPT augments the filter unless the step is f-type with the Armijo condition
+      if (!take_anyway && (flags & LSR_AUG)) filter_add((T(1) - g_th) * uth, uph - g_ph * uth);
       if (trace && ln == 0 && it < trace_cap - 2) {
         double* tr = trace + 8 * it;
         tr[0] = (double)kkt; tr[1] = (double)mu; tr[2] = (double)alpha; tr[3] = (double)ad;
-        tr[4] = (double)delta; tr[5] = (double)th; tr[6] = (double)ph;
-        tr[7] = (double)(take_anyway ? -100 - cw()->wd_trial : (accepted ? nls : -1));
+        tr[4] = (double)delta; tr[5] = (double)uth; tr[6] = (double)uph;
+        tr[7] = (double)(take_anyway ? -100 - cw()->wd_trial : (soc_taken ? 100 + nls : nls));
       }
       alpha_p = alpha;
       alpha_d = ad;
@@ -1897,6 +2536,14 @@ struct WaveSolver {
       tr[4] = (double)pr_max; tr[5] = (double)sc; tr[6] = (double)mu; tr[7] = 1000.0 + out.status;
     }
     return out;
+  }
+  MR_HD T alpha_min_of(T th, T gphi) const {
+    T a = T(1e-5);
+    if (gphi < T(0)) {
+      a = mr_min(a, T(1e-5) * th / (-gphi));
+      if (th <= theta_min) a = mr_min(a, mr_exp(T(1.1) * mr_log(mr_max(th, T(1e-30)))) / mr_exp(T(2.3) * mr_log(-gphi)));
+    }
+    return T(0.05) * a;
   }
 };
 
@@ -2022,6 +2669,7 @@ MR_HD void run_instance(Solver& S, const mr_inputs& in, const mr_outputs& out, i
   const Inst<T>& I = S.I;
   if (out.trace && out.trace_instance == i) { S.trace = out.trace; S.trace_cap = out.trace_cap; }
   S.init(in.u_init ? in.u_init + i : nullptr, B);
+  S.ls_init();
   SolveOut r = S.solve();
   const T viol = S.lane_violation();
   // outputs (the ret tuple of control/MPC.py:166-171), lane k writes stage k, global coordinates

@@ -407,6 +407,28 @@ class MPCProblem:
                 out.append(lhi[r] - llo[r])
         return np.array(out, dtype=np.float64)
 
+    def lam_g_ipopt(self, nu, yd):
+        """oracle.ipopt.solve_ipopt's multipliers (``nu`` on ``g``, ``yd`` on the ``ipopt_ineq`` rows, IPOPT's
+        sign: positive at an active upper bound) as the reference's ``opti.lam_g`` (MPC.py:171) in
+        ``opti_rows`` order.  A two-bounded ``opti.bounded`` row carries one multiplier, as in CasADi; the
+        lane rows are not Opti rows of the reference and are dropped."""
+        N = self.N
+        _d, _lo, _hi, kinds = self.ipopt_ineq()
+        yd = np.asarray(yd)
+        k = np.array(kinds)
+        by = {kind: yd[k == kind] for kind in dict.fromkeys(kinds)}
+        out = list(np.asarray(nu[:7]))
+        for i in range(1, N + 1):
+            out += list(np.asarray(nu[7 + 6 * (i - 1):7 + 6 * i]))
+            out.append(by["ds"][i - 1])
+        for i in range(N):
+            out += [by["thr_hi"][i], by["thr_lo"][i], by["steer_hi"][i], by["steer_lo"][i], by["dthr"][i],
+                    by["dsteer"][i]]
+        for kind in ("thr0", "steer0"):
+            if kind in by:
+                out.append(by[kind][0])
+        return np.array(out, dtype=np.float64)
+
     def push(self):
         """IPOPT-style slack push per one-sided row (kappa = 1e-2)."""
         rng = np.concatenate([self.hi - self.lo, self.hi - self.lo])

@@ -5,8 +5,10 @@ TEST FIXTURE GENERATOR (build container only; the GPU box never runs the oracle'
 For config 1 (C1dyn: the reference's dynamic model, C1kin: the kinematic variant; one instance) and
 each of C2, C3 (hard lane rows), C4 and C5 the first 32 instances of the config's batch
 (mpcracing.workload.make_batch, deterministic) are solved in fp64 by oracle.ipopt.solve_ipopt -- the
-dense restatement of IPOPT's algorithm with the watchdog and the restoration phase -- to a KKT tolerance
-of 1e-10, and the ret tuple of control/MPC.py:166-171 (States, U, S_hat, e_C, e_L), the objective, the
+dense restatement of IPOPT's algorithm with the watchdog and the restoration phase, under the rules the
+product restates (``ipopt.PRODUCT``; among them IPOPT's bound_relax_factor 1e-8, so active bounds sit
+1e-8 max(1, |b|) outside their nominal value, as in IPOPT's own solutions) -- to a KKT tolerance of 1e-10,
+and the ret tuple of control/MPC.py:166-171 (States, U, S_hat, e_C, e_L), the objective, the
 status and the iteration count are stored with the instance inputs.  tests/test_gpu_golden.py compares
 the GPU's fp64 solves of the same inputs with them.
 
@@ -48,7 +50,7 @@ def _solve(args):
     torch.set_num_threads(1)
     from mpcracing import workload as wl
     from oracle.nlp import MPCProblem
-    from oracle.ipopt import solve_ipopt
+    from oracle.ipopt import PRODUCT, solve_ipopt
     name, i = args
     cfg, b = _config(name)
     tyres = wl.tyre_coeffs(cfg["tyres"]) if cfg["tyres"] else None
@@ -56,7 +58,7 @@ def _solve(args):
     p = MPCProblem(inst["state0"], inst["s0"], inst["cx"], inst["cy"], inst["max_error"], N=cfg["N"], Ts=cfg["Ts"],
                    model=cfg["model"], lane_bounds=cfg["lane"], tyres=tyres)
     t0 = time.time()
-    r = solve_ipopt(p, tol=TOL, max_iter=1000, acceptable_iter=0, log=True)
+    r = solve_ipopt(p, tol=TOL, max_iter=1000, acceptable_iter=0, log=True, rules=PRODUCT)
     X, U, S, eC, eL = p.unpack(r.w)
     n_resto = sum(1 for e in r.log if e[7])
     return dict(i=i, status=r.status, iters=r.iters, resto_iters=n_resto, obj=r.obj, kkt=r.kkt, X=X, U=U, S=S,
@@ -81,7 +83,7 @@ def main():
             if v is not None:
                 out["in_" + k] = v
         np.savez_compressed(os.path.join(HERE, f"solutions_{name}.npz"), **out)
-        summ = {"config": name, "n": _n(name), "tol": TOL, "status": out["status"].tolist(),
+        summ = {"config": name, "n": _n(name), "tol": TOL, "rules": "PRODUCT", "status": out["status"].tolist(),
                 "iters": out["iters"].tolist(), "resto_iters": out["resto_iters"].tolist(),
                 "seconds": [round(r["t"], 1) for r in rs]}
         print(json.dumps(summ), flush=True)

@@ -2,14 +2,16 @@
 thread, OpenMP over instances -- what bench.py's cpu_baseline times) against the oracle.
 
 Same parity bar as the GPU tests (tests/test_gpu.py): fp64 at KKT tol 1e-10, controls / states /
-progress / errors within 1e-6 of the oracle's NLP solution (U[0, N-1] and vx_N excluded: only the
+progress / errors within 1e-6 of the oracle's IPOPT solution (oracle.ipopt.solve_ipopt, the product's rules:
+bounds relaxed by IPOPT's bound_relax_factor) (U[0, N-1] and vx_N excluded: only the
 barrier fixes them), objective within 1e-8 relative."""
 import numpy as np
 import pytest
 
 import host_twin as ht
 from mpcracing import workload as wl
-from oracle.nlp import MPCProblem, solve_ipm
+from oracle.ipopt import PRODUCT, solve_ipopt
+from oracle.nlp import MPCProblem
 
 
 @pytest.mark.parametrize("name,n,model", [("C1", 1, "kin"), ("C1", 1, "dyn"), ("C2", 2, None), ("C4", 1, None)])
@@ -24,7 +26,7 @@ def test_scalar_solver_vs_oracle(name, n, model):
         assert o["status"][i] == 0
         p = MPCProblem(inst["state0"], inst["s0"], inst["cx"], inst["cy"], inst["max_error"], N=cfg["N"],
                        Ts=cfg["Ts"], model=cfg["model"])
-        r = solve_ipm(p, tol=1e-10)
+        r = solve_ipopt(p, tol=1e-10, max_iter=1000, acceptable_iter=0, rules=PRODUCT)
         X, U, S, eC, eL = p.unpack(r.w)
         dU = np.abs(U - o["U"][:, :, i])
         dU[0, -1] = 0.0

@@ -1,8 +1,9 @@
 """The reference's dual output, ``opti.lam_g`` (control/MPC.py:171), from the solver's stage-wise multipliers.
 
 Bar: at fp64 tol 1e-10 the exported lam_g [13N+9] equals the oracle's multipliers mapped to the
-reference's Opti rows (oracle.nlp.MPCProblem.lam_g; row order pinned against the reference's own
-constraint recording in tests/test_nlp_golden.py) to 1e-7 relative to max |lam_g|.  CasADi's sign
+reference's Opti rows (oracle.ipopt.solve_ipopt under the product's rules, oracle.nlp.MPCProblem.lam_g_ipopt; row
+order pinned against the reference's own constraint recording in tests/test_nlp_golden.py) to 1e-7 relative
+to max |lam_g|.  CasADi's sign
 convention: Lagrangian f + lam_g . g with the canonical Opti rows (stated, not pinned: no casadi here).
 CPU test: the host build of the kernel source (emulated wavefront); GPU test: libmpcracing.so."""
 import numpy as np
@@ -10,14 +11,15 @@ import pytest
 
 import host_twin as ht
 from mpcracing import workload as wl
-from oracle.nlp import MPCProblem, solve_ipm
+from oracle.ipopt import PRODUCT, solve_ipopt
+from oracle.nlp import MPCProblem
 
 
 def _oracle_lam(cfg, inst, model, N, Ts):
     p = MPCProblem(inst["state0"], inst["s0"], inst["cx"], inst["cy"], inst["max_error"], N=N, Ts=Ts, model=model)
-    r = solve_ipm(p, tol=1e-10)
+    r = solve_ipopt(p, tol=1e-10, max_iter=1000, acceptable_iter=0, rules=PRODUCT)
     assert r.status == 0
-    return p.lam_g(r.nu, r.lam)
+    return p.lam_g_ipopt(r.nu, r.lam)
 
 
 def _check(lg, mine):
@@ -49,8 +51,8 @@ def test_lam_g_state0_controls_none():
     lc = [(0.0, 0.0)] + cols[:-1]  # MPCProblem shifts last_controls itself: lc[1:] + [lc[-1]] == cols
     p = MPCProblem(inst["state0"], inst["s0"], inst["cx"], inst["cy"], inst["max_error"], N=20, Ts=0.1, model="dyn",
                    last_controls=lc)
-    r = solve_ipm(p, tol=1e-10)
-    _check(p.lam_g(r.nu, r.lam), o["lam_g"][:, 0])
+    r = solve_ipopt(p, tol=1e-10, max_iter=1000, acceptable_iter=0, rules=PRODUCT)
+    _check(p.lam_g_ipopt(r.nu, r.lam), o["lam_g"][:, 0])
 
 
 @pytest.mark.gpu
