@@ -135,6 +135,10 @@ typedef struct mr_outputs {
                       bound); unscaled objective.  NULL to skip. */
   int64_t* timeline; /* optional [2][B] diagnostics: device clock (s_memrealtime, 100 MHz) when instance i's
                         workgroup started and finished; NULL to skip */
+  double* constr_viol; /* optional [B]: IPOPT's unscaled constraint violation of the returned point (max-norm
+                          of the dynamics / initial-state rows and of the rows' bound violations; the
+                          "Constraint violation" IPOPT prints on exit).  Tells a status-3 stop at an
+                          almost-feasible point from a restoration failure.  NULL to skip */
 } mr_outputs;
 
 typedef struct mr_handle mr_handle;

@@ -14,8 +14,16 @@ Differences that are visible to a caller:
   * ``dual`` is the reference's ``opti.lam_g`` (MPC.py:171): one multiplier per
     constraint row in Opti order, CasADi's sign convention (include/mpcracing.h
     ``lam_g``); ``None`` on failure, as the reference.
-  * the solver is a primal-dual interior-point method with IPOPT's rules, run to
-    tol 1e-8 (the reference's IPOPT tol is 1e-4).
+  * the solver is a primal-dual interior-point method with IPOPT's rules, run with
+    the reference's IPOPT options (MPC.py:152-161: tol 1e-4, acceptable_tol 1e-2,
+    IPOPT's acceptable_iter 15, max_iter FixedControllerParameters.max_iter) unless
+    the keyword-only ``tol`` / ``acceptable_tol`` / ``acceptable_iter`` say otherwise.
+    IPOPT's termination tests are unscaled (compl_inf_tol 1e-4, acceptable 1e-2):
+    with the gradient-based objective scaling of a cold start (the S_hat guess at
+    top speed, MPC.py:127, makes |grad f| ~ 1e5 and df ~ 1e-4) the unscaled
+    complementarity at IPOPT's mu floor (tol / 11) stays above both, and the solve
+    ends as IPOPT's does -- restoration failure at an almost-feasible point -- so
+    ``sol`` is None there, exactly as the reference's except branch.
 """
 from dataclasses import dataclass
 import math
@@ -48,18 +56,25 @@ def _fixed_fields(fp):
                 max_iter=int(FixedControllerParameters.max_iter))
 
 
-def get_solver(N, Ts, model="dyn", lane_bounds=False, precision="fp64", max_batch=1, device=0, tyres=None):
+# the reference's IPOPT options (control/MPC.py:152-161; acceptable_iter is IPOPT's default)
+REFERENCE_OPTIONS = dict(tol=1e-4, acceptable_tol=1e-2, acceptable_iter=15)
+
+
+def get_solver(N, Ts, model="dyn", lane_bounds=False, precision="fp64", max_batch=1, device=0, tyres=None,
+               tol=REFERENCE_OPTIONS["tol"], acceptable_tol=REFERENCE_OPTIONS["acceptable_tol"],
+               acceptable_iter=REFERENCE_OPTIONS["acceptable_iter"]):
     """Cached BatchSolver for one NLP configuration (the reference rebuilds its NLP every call;
     here the handle and its workspace are reused, only the data changes)."""
     from mpcracing.batch import BatchSolver
     fp = FixedControllerParameters()
+    opts = dict(tol=float(tol), acceptable_tol=float(acceptable_tol), acceptable_iter=int(acceptable_iter))
     key = (int(N), float(Ts), model, bool(lane_bounds), precision, int(max_batch), int(device),
            tuple(sorted(config_fields().items())), tuple(sorted(_fixed_fields(fp).items())),
-           None if tyres is None else repr(tyres))
+           None if tyres is None else repr(tyres), tuple(sorted(opts.items())))
     s = _solvers.get(key)
     if s is None:
         s = BatchSolver(N, model, precision, lane_bounds, Ts, max_batch=max_batch, device=device, tyres=tyres,
-                        **config_fields(), **_fixed_fields(fp))
+                        **opts, **config_fields(), **_fixed_fields(fp))
         _solvers[key] = s
     return s
 
@@ -68,10 +83,11 @@ class MPCBatch:
     """Solve B MPC instances at once.  Arrays follow include/mpcracing.h (instance index last)."""
 
     def __init__(self, N, Ts=None, model="dyn", lane_bounds=False, precision="fp64", max_batch=1024, device=0,
-                 tyres=None):
+                 tyres=None, **options):
         Ts = FixedControllerParameters.Ts if Ts is None else Ts
         self.N = int(N)
-        self.solver = get_solver(N, Ts, model, lane_bounds, precision, max_batch, device, tyres)
+        self.solver = get_solver(N, Ts, model, lane_bounds, precision, max_batch, device, tyres,
+                                 **dict(REFERENCE_OPTIONS, **options))
 
     def solve(self, state0, s0, cx, cy, max_error, runtime, u_init=None):
         out = self.solver.solve(dict(state0=state0, s0=s0, cx=cx, cy=cy, max_error=max_error, runtime=runtime,
@@ -82,7 +98,9 @@ class MPCBatch:
 class MPC:
     def __init__(self, state0, s0, centerline_x_poly_coeffs, centerline_y_poly_coeffs, max_error,
                  runtime_params, sol0=None, duals=None, last_controls=None, Ts=None, N=None, *,
-                 model="dyn", lane_bounds=False, device=0):
+                 model="dyn", lane_bounds=False, device=0, tol=REFERENCE_OPTIONS["tol"],
+                 acceptable_tol=REFERENCE_OPTIONS["acceptable_tol"],
+                 acceptable_iter=REFERENCE_OPTIONS["acceptable_iter"]):
         # sol0 / duals are accepted and ignored, as in the reference (MPC.py:17-18)
         self.fixed_params = FixedControllerParameters()
         self.runtime_params = runtime_params
@@ -110,7 +128,8 @@ class MPC:
             runtime=np.array(_runtime_row(runtime_params), dtype=np.float64).reshape(5, 1),
             u_init=u_init,
         )
-        solver = get_solver(N, Ts, model, lane_bounds, device=device)
+        solver = get_solver(N, Ts, model, lane_bounds, device=device, tol=tol, acceptable_tol=acceptable_tol,
+                            acceptable_iter=acceptable_iter)
         out = {k: v.cpu().numpy() for k, v in solver.solve(batch, duals=True).items()}
         status = int(out["status"][0])
         from mpcracing.abi import STATUS

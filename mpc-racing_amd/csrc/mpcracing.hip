@@ -158,9 +158,7 @@ __device__ __forceinline__ int order_scan(int* cnt, int t, int c) {  // inclusiv
   __syncthreads();
   return r;
 }
-__global__ __launch_bounds__(kOrderThreads) void mr_order_kernel(const double* state0, int B, int* order) {
-  __shared__ int cnt[kOrderThreads];
-  __shared__ int tot[2];
+__device__ void order_tiers(const double* state0, int B, int* order, int* cnt, int* tot) {
   const int t = threadIdx.x;
   const int per = (B + kOrderThreads - 1) / kOrderThreads;
   const int lo = min(B, t * per), hi = min(B, lo + per);
@@ -185,21 +183,34 @@ __global__ __launch_bounds__(kOrderThreads) void mr_order_kernel(const double* s
     else order[p2++] = i;
   }
 }
+__global__ __launch_bounds__(kOrderThreads) void mr_order_kernel(const double* state0, int B, int* order) {
+  __shared__ int cnt[kOrderThreads];
+  __shared__ int tot[2];
+  order_tiers(state0, B, order, cnt, tot);
+}
 
 // dispatch_order = 2: workgroups take instances in decreasing order_hint (longest expected first), e.g.
 // the previous MPC tick's iteration counts.  One workgroup: bucket histogram (hint clamped to
 // 0..kHintBuckets-1) in LDS, a scan from the largest bucket down, then an atomic scatter (the order within
-// a bucket is arbitrary; results do not depend on the order).
+// a bucket is arbitrary; results do not depend on the order).  A hint that says nothing (every instance in
+// one bucket, e.g. all zero on a first tick) falls back to dispatch_order 1's distribution-agnostic tiers.
 constexpr int kHintBuckets = kOrderThreads;
 __device__ __forceinline__ int hint_bucket(int h) { return h < 0 ? 0 : (h >= kHintBuckets ? kHintBuckets - 1 : h); }
-__global__ __launch_bounds__(kOrderThreads) void mr_order_hint_kernel(const int32_t* hint, int B, int* order) {
+__global__ __launch_bounds__(kOrderThreads) void mr_order_hint_kernel(const int32_t* hint, const double* state0,
+                                                                      int B, int* order) {
   __shared__ int cnt[kHintBuckets];
   __shared__ int scan[kOrderThreads];
+  __shared__ int tot[2];
   const int t = threadIdx.x;
   cnt[t] = 0;
   __syncthreads();
   for (int i = t; i < B; i += kOrderThreads) atomicAdd(&cnt[hint_bucket(hint[i])], 1);
   __syncthreads();
+  if (cnt[hint_bucket(hint[0])] == B) {  // uniform hint: block-uniform branch
+    __syncthreads();
+    order_tiers(state0, B, order, scan, tot);
+    return;
+  }
   const int r = kHintBuckets - 1 - t;  // thread t scans bucket r: the largest bucket first
   const int c = cnt[r];
   const int incl = order_scan(scan, t, c);
@@ -234,8 +245,13 @@ static int launch(mr_handle* h, int B, const mr_inputs* in, mr_outputs* out, hip
     hipLaunchKernelGGL(mr_order_kernel, dim3(1), dim3(kOrderThreads), 0, st, in->state0, B, h->order);
     HIP_TRY(hipGetLastError());
     order = h->order;
-  } else if (h->cfg.dispatch_order == 2 && in->order_hint && B > 1) {
-    hipLaunchKernelGGL(mr_order_hint_kernel, dim3(1), dim3(kOrderThreads), 0, st, in->order_hint, B, h->order);
+  } else if (h->cfg.dispatch_order == 2 && B > 1) {
+    // without a hint: dispatch_order 1's tiers
+    if (in->order_hint)
+      hipLaunchKernelGGL(mr_order_hint_kernel, dim3(1), dim3(kOrderThreads), 0, st, in->order_hint, in->state0, B,
+                         h->order);
+    else
+      hipLaunchKernelGGL(mr_order_kernel, dim3(1), dim3(kOrderThreads), 0, st, in->state0, B, h->order);
     HIP_TRY(hipGetLastError());
     order = h->order;
   }
@@ -517,14 +533,24 @@ int mr_destroy(mr_handle* h) {
 
 int mr_set_tyres(mr_handle* h, const double* a_front, double Fz_front, const double* a_back, double Fz_back) {
   if (!h || !a_front || !a_back) return fail(MR_ERR_ARG, "null argument");
-  h->tf = pacejka_coef(a_front, Fz_front);
-  h->tr = pacejka_coef(a_back, Fz_back);
-  h->have_tyres = 1;
   MR_GUARD_DEVICE(h->cfg.device);
   // the kernels read the constants from this buffer while they run: a solve still in flight on any
   // stream of the device (torch side streams do not order with the copy below) must finish first
   HIP_TRY(hipDeviceSynchronize());
-  return upload_params(h);
+  // the handle takes the new coefficients only once they are on the device
+  const auto tf = h->tf, tr = h->tr;
+  const int had = h->have_tyres;
+  h->tf = pacejka_coef(a_front, Fz_front);
+  h->tr = pacejka_coef(a_back, Fz_back);
+  const int rc = upload_params(h);
+  if (rc != MR_OK) {
+    h->tf = tf;
+    h->tr = tr;
+    h->have_tyres = had;
+    return rc;
+  }
+  h->have_tyres = 1;
+  return MR_OK;
 }
 
 int64_t mr_workspace_bytes_per_instance(const mr_handle* h) {

@@ -98,6 +98,7 @@ MR_HD SolveOut solve_instance(const ProbParams<T>& P, const mr_inputs& in, const
   out.iters[i] = r.iters;
   if (out.obj) out.obj[i] = r.obj - (double)P.lambda_s * s0;  // -lambda_s * S_N in global s
   if (out.kkt) out.kkt[i] = r.kkt;
+  if (out.constr_viol) out.constr_viol[i] = r.viol;
   return r;
 }
 

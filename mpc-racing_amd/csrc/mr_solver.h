@@ -678,6 +678,7 @@ constexpr double RESTO_RHO = 1000.0, RESTO_KAPPA = 0.9, RESTO_MULT_RESET = 1000.
 struct SolveOut {
   int status, iters;
   double kkt, obj;
+  double viol;  // IPOPT's unscaled constraint violation of the returned point (max-norm, mr_outputs.constr_viol)
 };
 
 #ifndef MR_FMAX
@@ -1936,6 +1937,7 @@ struct Solver {
       for (int i = 0; i < NX; ++i) { nub[k][i] = wnub[k][i]; W(k, WF::DNU + i) = W(k, WF::WDNU + i); }
     }
   }
+  double acc_kkt = 0.0, acc_obj = 0.0, acc_viol = 0.0;  // the stored acceptable point's measures
   MR_HD void acc_save() {  // IPOPT's backup acceptable iterate (primal part: what the solve returns)
     for (int k = 0; k <= N; ++k)
       for (int i = 0; i < NZS; ++i) W(k, WF::AZ + i) = W(k, zf(cur) + i);
@@ -1969,8 +1971,34 @@ struct Solver {
     delta_last_o = delta_last;
     theta_max_o = theta_max;
     theta_min_o = theta_min;
-    const T mu_r = mr_max(mu, pr_max);
-    T th_rows = T(0);
+    // the current point's constraint values, measured here: after a watchdog restore the evaluation
+    // sweep's (defects W(k, C), pr_max, theta) belong to the abandoned iterate.  IPOPT's
+    // RestoIterateInitializer: mu_r = max(mu, ||c||_inf, ||d - s||_inf)
+    T pr = T(0), th_r = T(0);
+    for (int k = 0; k <= N; ++k) {
+      T z[NZS];
+      load_z(k, cur, z);
+      if (k < N) {
+        T zn[NZS], xn[NX];
+        load_z(k + 1, cur, zn);
+        faug<T, MODEL>(P, k, z, xn);
+        for (int i = 0; i < NX; ++i) {
+          const T c = xn[i] - zn[i];
+          W(k, WF::C + i) = c;
+          pr = mr_max(pr, mr_abs(c));
+          if (i >= 6) th_r += mr_abs(c);  // definitional rows (S, previous controls): not relaxed
+        }
+      }
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      T d[NI];
+      int act[NI];
+      Row<T> rows[NROW];
+      row_values(k, z, e, d, act, rows);
+      for (int j = 0; j < NI; ++j)
+        if (act[j] && yslot(j)) pr = mr_max(pr, mr_abs(d[j] - W(k, sf(cur) + j)));
+    }
+    const T mu_r = mr_max(mu, pr);
     for (int k = 0; k <= N; ++k) {
       T z[NZS];
       load_z(k, cur, z);
@@ -1985,11 +2013,7 @@ struct Solver {
         T p = T(1), n = T(1);
         W(k, WF::RS0 + j) = W(k, sf(cur) + j);
         W(k, WF::RLAM + j) = W(k, WF::LAM + j);
-        if (act[j]) {
-          const T c = d[j] - W(k, sf(cur) + j);
-          if (yslot(j)) th_rows += mr_abs(c);
-          resto_pn(c, mu_r, rho, p, n);
-        }
+        if (act[j]) resto_pn(d[j] - W(k, sf(cur) + j), mu_r, rho, p, n);
         W(k, WF::RP + j) = p;
         W(k, WF::RN + j) = n;
         W(k, WF::RVP + j) = mu_r / p;
@@ -2004,9 +2028,7 @@ struct Solver {
       if (k < N)
         for (int i = 0; i < 6; ++i) {  // the vehicle rows start satisfied too (p - n = F - x')
           T p, n;
-          const T c = W(k, WF::C + i);
-          th_rows += mr_abs(c);
-          resto_pn(c, mu_r, rho, p, n);
+          resto_pn(W(k, WF::C + i), mu_r, rho, p, n);
           W(k, WF::CP + i) = p;
           W(k, WF::CN + i) = n;
           W(k, WF::CVP + i) = mu_r / p;
@@ -2019,7 +2041,6 @@ struct Solver {
     resto = true;
     nfilt = 0;
     delta_last = T(0);
-    const T th_r = mr_max(theta - th_rows, T(0));  // relaxed rows start satisfied: the definitional rows only
     theta_max = T(1e4) * mr_max(T(1), th_r);
     theta_min = T(1e-4) * mr_max(T(1), th_r);
   }
@@ -2127,7 +2148,7 @@ struct Solver {
     const T kappa_eps = T(10), kappa_mu = T(0.2), theta_mu = T(1.5);
     // IPOPT's monotone update keeps mu >= min(tol, compl_inf_tol) / (barrier_tol_factor + 1)
     const T mu_min = mr_max(T(1e-11), mr_min(P.tol, T(IP_COMPL_INF_TOL)) / (kappa_eps + T(1)));
-    SolveOut out{2, 0, 0.0, 0.0};
+    SolveOut out{2, 0, 0.0, 0.0, 0.0};
     T mu_prev = mu;
     int acc_count = 0;
     // IPOPT's filter reset heuristic (filter_reset_trigger = 5, max_filter_resets = 5): after this many
@@ -2151,10 +2172,12 @@ struct Solver {
         // the restoration NLP converged at a point the original problem does not accept: IPOPT's
         // "restoration converged to a feasible point unacceptable to the filter" (restoration failed)
         // when that point is feasible to 1e2 tol, else "converged to a point of local infeasibility"
+        out.viol = (double)mr_max(pr_o, viol_max);  // the restoration iterate as the original problem sees it
         if (kkt <= P.tol) { out.status = pr_o <= T(100) * P.tol ? 3 : MR_STATUS_INFEASIBLE; break; }
       } else {
         out.kkt = (double)kkt;
         out.obj = (double)(fval / sc);
+        out.viol = (double)mr_max(pr_eq, viol_max);
         if (converged(kkt)) { out.status = 0; break; }
         if (P.acc_iter > 0) {
           acc_count = acceptable(kkt) ? acc_count + 1 : 0;
@@ -2251,7 +2274,10 @@ struct Solver {
         }
         continue;
       }
-      if (acceptable(kkt)) acc_save();  // IPOPT stores the current iterate if it is acceptable
+      if (acceptable(kkt)) {  // IPOPT stores the current iterate if it is acceptable
+        acc_save();
+        acc_kkt = out.kkt; acc_obj = out.obj; acc_viol = out.viol;
+      }
 #if MR_WD_TRIGGER > 0
       // IPOPT's watchdog (watchdog_shortened_iter_trigger, watchdog_trial_iter_max): after that many
       // successive iterations whose accepted step was shorter than the fraction-to-boundary step, store
@@ -2312,7 +2338,13 @@ struct Solver {
         // -> the stored acceptable point, or restoration failed; otherwise the restoration phase
         if (acceptable(kkt)) { out.status = 1; break; }
         if (theta <= T(1e-2) * P.tol) {
-          if (have_acc) { acc_restore(); out.status = 1; } else { out.status = 3; }
+          if (have_acc) {
+            acc_restore();
+            out.status = 1;
+            out.kkt = acc_kkt; out.obj = acc_obj; out.viol = acc_viol;
+          } else {
+            out.status = 3;
+          }
           break;
         }
         resto_enter(th, ph);

@@ -293,7 +293,7 @@ struct WaveSolver {
   double* trace = nullptr;
   int trace_cap = 0;
 #if MR_PHASE_CYCLES
-  unsigned long long tsub[6] = {0, 0, 0, 0, 0, 0};  // diagnostics: sub-phase cycles of the trace instance
+  unsigned long long tsub[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // diagnostics: sub-phase cycles of the trace instance
 #endif
 
   MR_HD WaveSolver(const MR_CONST ProbParams<T>& P_, const Inst<T>& I_, Wv w_, MR_GLOBAL T* ws, MR_LDS T* lds_,
@@ -1060,7 +1060,7 @@ struct WaveSolver {
   // factorisation, and a smaller record).
   // Restoration phase: the cost-to-go tile P^ of stage k+1 (LP) minimised over the disturbance of
   // stage k's relaxed vehicle rows (mr_solver.h noise_cond): M = P_vv + diag(sw) = L L^T (every lane,
-  // registers), Y = L^-1 [P_v. | p0_v + gw0 | p1_v + gw1] (lane c < 13: column c, to the LX scratch
+  // registers), Y = L^-1 [P_v. | p_v + gw0 + mu gw1] (lane c < 12: column c, to the LX scratch
   // tile), then P^ -= Y^T Y entry-wise.  False if M is not positive definite.
   // In fp64 whatever T (mr_solver.h noise_cond: the vehicle block of P^ is otherwise fp32 rounding noise
   // where a relaxation is active); the L^-1 columns go through the LX scratch tile as doubles.
@@ -1080,15 +1080,17 @@ struct WaveSolver {
       for (int j = 0; j < 6; ++j) M[i * 6 + j] = (D)LP[i * LDS_LD + j] + (i == j ? sw[i] : 0.0);
     const bool ok = chol6(M, L);
     if (!wuni(w, ok)) return false;
-    const int c = l < 13 ? l : 0;
+    // 12 columns: the 11 states and the right-hand side (mu folded in, column 11); the tile's column 12
+    // is not part of the wave Riccati's record
+    const int c = l < 12 ? l : 0;
     D col[6];
     for (int i = 0; i < 6; ++i) col[i] = (D)LP[i * LDS_LD + c] + (c == 11 ? gw0[i] + (D)mu * gw1[i] : 0.0);
     lsolve6(L, col);
-    if (l < 13)
+    if (l < 12)
       for (int a = 0; a < 6; ++a) LX[a * 16 + l] = col[a];
     wsync_lds(w);
-    for (int e = l; e < NX * 13; e += WL) {
-      const int i = e / 13, j = e - 13 * (e / 13);
+    for (int e = l; e < NX * 12; e += WL) {
+      const int i = e / 12, j = e - 12 * (e / 12);
       D v = (D)LP[i * LDS_LD + j];
       for (int a = 0; a < 6; ++a) v -= LX[a * 16 + i] * LX[a * 16 + j];
       LP[i * LDS_LD + j] = (T)v;
@@ -2097,26 +2099,42 @@ struct WaveSolver {
     C->theta_max_o = theta_max;
     C->theta_min_o = theta_min;
     C->rho = rho;
-    const T mu_r = mr_max(mu, pr_max);
-    T th_rows_l = T(0);
+    // the current point's constraint values, measured here: after a watchdog restore the evaluation
+    // sweep's (defects in the stage record, pr_max, theta) belong to the abandoned iterate
+    const int k = ln;
+    T z[NZS];
+    load_z(cur, z);
+    T znext[NX], c[NX], d[NI];
+    int act[NI];
+    for (int i = 0; i < NX; ++i) { znext[i] = wnext(w, z[i]); c[i] = T(0); }
+    T pr_l = T(0), th_def_l = T(0);
     if (own()) {
-      const int k = ln;
-      T z[NZS];
-      load_z(cur, z);
-      for (int i = 0; i < NZS; ++i) Cf(CSF::RZ + i) = z[i];
+      if (k < N) {
+        T xn[NX];
+        faug<T, MODEL>(P, k, z, xn);
+        for (int i = 0; i < NX; ++i) {
+          c[i] = xn[i] - znext[i];
+          pr_l = mr_max(pr_l, mr_abs(c[i]));
+          if (i >= 6) th_def_l += mr_abs(c[i]);  // definitional rows (S, previous controls): not relaxed
+        }
+      }
       Err<T> e;
       errors(I, z[0], z[1], z[6], e, false);
-      T d[NI];
-      int act[NI];
       row_values(k, z, e, d, act);
+      for (int j = 0; j < NI; ++j)
+        if (act[j] && yslot(j)) pr_l = mr_max(pr_l, mr_abs(d[j] - S(sf(cur) + j)));
+    }
+    // IPOPT's RestoIterateInitializer: mu_r = max(mu, ||c||_inf, ||d - s||_inf)
+    const T mu_r = mr_max(mu, wmax(w, pr_l));
+    const T th_r = wsum(w, th_def_l);  // relaxed rows start satisfied: the definitional rows only
+    if (own()) {
+      for (int i = 0; i < NZS; ++i) Cf(CSF::RZ + i) = z[i];
       for (int j = 0; j < NI; ++j) {
         T p = T(1), n = T(1);
         Cf(CSF::RS0 + j) = S(sf(cur) + j);
         Cf(CSF::RLAM + j) = S(SSF::LAM + j);
         if (act[j]) {
-          const T s = S(sf(cur) + j), c = d[j] - s;
-          if (yslot(j)) th_rows_l += mr_abs(c);
-          resto_pn(c, mu_r, rho, p, n);
+          resto_pn(d[j] - S(sf(cur) + j), mu_r, rho, p, n);
           // the slacks' bound duals: the original problem's, but not above rho (RestoIterateInitializer)
           S(SSF::LAM + j) = mr_min(S(SSF::LAM + j), rho);
         }
@@ -2133,9 +2151,7 @@ struct WaveSolver {
       if (k < N)
         for (int i = 0; i < 6; ++i) {  // the vehicle rows start satisfied too (p - n = F - x')
           T p, n;
-          const T c = R(k)[RCF::C + i];
-          th_rows_l += mr_abs(c);
-          resto_pn(c, mu_r, rho, p, n);
+          resto_pn(c[i], mu_r, rho, p, n);
           Cf(CSF::CP + i) = p;
           Cf(CSF::CN + i) = n;
           Cf(CSF::CVP + i) = mu_r / p;
@@ -2143,13 +2159,11 @@ struct WaveSolver {
           Cf(CSF::CDP + i) = T(0); Cf(CSF::CDN + i) = T(0); Cf(CSF::CDVP + i) = T(0); Cf(CSF::CDVN + i) = T(0);
         }
     }
-    const T th_rows = wsum(w, th_rows_l);
     alpha_p = alpha_d = T(0);
     mu = mu_r;
     C->resto = 1;
     nfilt = 0;
     delta_last = T(0);
-    const T th_r = mr_max(theta - th_rows, T(0));  // relaxed rows start satisfied: the definitional rows only
     theta_max = T(1e4) * mr_max(T(1), th_r);
     theta_min = T(1e-4) * mr_max(T(1), th_r);
     wsync(w);
@@ -2248,7 +2262,8 @@ struct WaveSolver {
     // IPOPT's monotone update keeps mu >= min(tol, compl_inf_tol) / (barrier_tol_factor + 1)
     const T mu_min = mr_max(T(1e-11), mr_min(P.tol, T(IP_COMPL_INF_TOL)) / (kappa_eps + T(1)));
     const T g_th = T(1e-5), g_ph = T(1e-5);
-    SolveOut out{2, 0, 0.0, 0.0};
+    SolveOut out{2, 0, 0.0, 0.0, 0.0};
+    double acc_kkt = 0.0, acc_obj = 0.0, acc_viol = 0.0;  // the stored acceptable point's measures
     T mu_prev = mu;
     int acc_count = 0;
     // IPOPT's filter reset heuristic (filter_reset_trigger = 5, max_filter_resets = 5): after this many
@@ -2267,6 +2282,12 @@ struct WaveSolver {
 #define MR_T1(slot) ((void)0)
 #define MR_CNT(slot) ((void)0)
 #endif
+#ifdef MR_WAVE_STATS
+    long st_trials = 0, st_soc_try = 0, st_soc_ok = 0, st_resto = 0, st_wd = 0, st_fact = 0, st_lsfail = 0;
+#define MR_STAT(x) (x)
+#else
+#define MR_STAT(x) ((void)0)
+#endif
     for (it = 0;; ++it) {
 #if MR_DEVICE_BUILD && MR_PRIO_ITER > 0
       // long solves: raise the wave's issue priority over the partner wave on its SIMD, so the
@@ -2283,10 +2304,12 @@ struct WaveSolver {
       if (rs) {
         // the restoration NLP converged at a point the original problem does not accept: restoration
         // failed when that point is feasible to 1e2 tol (IPOPT), else a point of local infeasibility
+        out.viol = (double)mr_max(cw()->pr_o, cw()->viol);  // the restoration iterate as the original problem sees it
         if (kkt <= P.tol) { out.status = cw()->pr_o <= T(100) * P.tol ? 3 : MR_STATUS_INFEASIBLE; break; }
       } else {
         out.kkt = (double)kkt;
         out.obj = (double)(fval / sc);
+        out.viol = (double)mr_max(cw()->pr_eq, cw()->viol);
         if (converged(kkt)) { out.status = 0; break; }
         if (P.acc_iter > 0) {
           acc_count = acceptable(kkt) ? acc_count + 1 : 0;
@@ -2319,6 +2342,7 @@ struct WaveSolver {
         if (trace && !rok) { tsub[4] += MR_CLOCK() - tr0; tsub[5] += 1; }
         if (rok) { fact_ok = true; break; }
 #else
+        MR_STAT(st_fact++);
         if (rs ? riccati<true>(delta, mu) : riccati<false>(delta, mu)) { fact_ok = true; break; }
 #endif
         if (first) {
@@ -2353,6 +2377,7 @@ struct WaveSolver {
         MR_T0();
         line_search<true, false>(th, ph, gphi, th_pow, ap, ap, a_min, 0, 0, T(0), T(-1));
         MR_T1(3);
+        MR_STAT((st_resto++, st_trials += res_ntr));
         if (!(res_flags & LSR_ACC)) { out.status = 3; break; }  // IPOPT: restoration failed
         if (res_flags & LSR_AUG) filter_add((T(1) - g_th) * th, ph - g_ph * th);
         if (trace && ln == 0 && it < trace_cap - 2) {
@@ -2375,7 +2400,10 @@ struct WaveSolver {
         }
         continue;
       }
-      if (acceptable(kkt)) acc_save();  // IPOPT stores the current iterate if it is acceptable
+      if (acceptable(kkt)) {  // IPOPT stores the current iterate if it is acceptable
+        acc_save();
+        acc_kkt = out.kkt; acc_obj = out.obj; acc_viol = out.viol;
+      }
 #if MR_WD_TRIGGER > 0
       // IPOPT's watchdog (mr_solver.h, same rule): after watchdog_shortened_iter_trigger successive
       // shortened steps store the iterate and direction, take full steps tentatively, judged against the
@@ -2441,9 +2469,20 @@ struct WaveSolver {
               line_search<false, false>(th, ph, gphi, th_pow, a_soc, ap, a_min, 0, LS_ACC, a_soc, a_soc);
             else
               line_search<false, true>(th, ph, gphi, th_pow, a_soc, ap, a_min, 0, LS_ACC, a_soc, a_soc);
+            MR_STAT(st_soc_try++);
+            MR_CNT(5);
+#if MR_PHASE_CYCLES
+            const unsigned long long ts0 = trace ? MR_CLOCK() : 0ull;
+#endif
             soc_backward();
+#if MR_PHASE_CYCLES
+            const unsigned long long ts1 = trace ? MR_CLOCK() : 0ull;
+#endif
             T aps, ads;
             forward_soc(aps, ads);
+#if MR_PHASE_CYCLES
+            if (trace) { tsub[6] += ts1 - ts0; tsub[7] += MR_CLOCK() - ts1; }
+#endif
             line_search<false, true>(th, ph, gphi, th_pow, aps, aps, aps, 0, LS_WD, a_test0, T(-1));
             rejf |= (res_flags & LSR_REJF) != 0;
             a_soc = aps;
@@ -2467,17 +2506,23 @@ struct WaveSolver {
       MR_T1(3);
 #if MR_PHASE_CYCLES
       cyc[4] += res_ntr;
-      cyc[5] += soc_taken ? 1 : 0;
 #endif
       alpha = res_alpha;
       const int nls = res_nls;
+      MR_STAT((st_trials += res_ntr, st_soc_ok += soc_taken, st_wd += take_anyway, st_lsfail += (!accepted && !take_anyway)));
       if (!accepted && !take_anyway) {
         // IPOPT on a failed line search (the soft restoration phase is not restated): the
         // current point acceptable -> "acceptable point reached"; almost feasible (theta <= 1e-2 tol) ->
         // the stored acceptable point or restoration failed; otherwise the restoration phase
         if (acceptable(kkt)) { out.status = 1; break; }
         if (theta <= T(1e-2) * P.tol) {
-          if (cw()->have_acc) { acc_restore(); out.status = 1; } else { out.status = 3; }
+          if (cw()->have_acc) {
+            acc_restore();
+            out.status = 1;
+            out.kkt = acc_kkt; out.obj = acc_obj; out.viol = acc_viol;
+          } else {
+            out.status = 3;
+          }
           break;
         }
         resto_enter(th, ph);
@@ -2518,6 +2563,12 @@ struct WaveSolver {
       wsync(w);  // new iterate buffer written by every lane before the next evaluation
     }
     out.iters = it;
+#ifdef MR_WAVE_STATS
+    if (ln == 0)
+      printf("wave stats: status %d iters %d trials %ld soc_try %ld soc_ok %ld resto %ld wd %ld fact %ld lsfail %ld\n",
+             out.status, it, st_trials, st_soc_try, st_soc_ok, st_resto, st_wd, st_fact, st_lsfail);
+#endif
+#undef MR_STAT
 #undef MR_T0
 #undef MR_T1
 #undef MR_CNT
@@ -2526,8 +2577,8 @@ struct WaveSolver {
       double* tr = trace + 8 * (trace_cap - 1);
       for (int q = 0; q < 7; ++q) tr[q] = (double)cyc[q];
       tr[7] = (double)(trace ? MR_CLOCK() - tstart : 0ull);
-      double* tr2 = trace + 8 * (trace_cap - 2);  // sub-phases: forward seq/par, eval stage/reduce, failed factorisations (cycles, count)
-      for (int q = 0; q < 6; ++q) tr2[q] = (double)tsub[q];
+      double* tr2 = trace + 8 * (trace_cap - 2);  // sub-phases: forward seq/par, eval stage/reduce, failed factorisations (cycles, count), SOC backward / forward
+      for (int q = 0; q < 8; ++q) tr2[q] = (double)tsub[q];
     }
 #endif
     if (trace && ln == 0 && it < trace_cap - 2) {
@@ -2697,6 +2748,7 @@ MR_HD void run_instance(Solver& S, const mr_inputs& in, const mr_outputs& out, i
     out.iters[i] = r.iters;
     if (out.obj) out.obj[i] = r.obj - (double)P.lambda_s * s0;
     if (out.kkt) out.kkt[i] = r.kkt;
+    if (out.constr_viol) out.constr_viol[i] = r.viol;
   }
 }
 

@@ -38,7 +38,8 @@ class MRInputs(ctypes.Structure):
 class MROutputs(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in ("X", "U", "S", "eC", "eL", "status", "iters", "obj", "kkt",
                                                "trace")] + [("trace_instance", _I32), ("trace_cap", _I32),
-                                                           ("lam_g", ctypes.c_void_p), ("timeline", ctypes.c_void_p)]
+                                                           ("lam_g", ctypes.c_void_p), ("timeline", ctypes.c_void_p),
+                                                           ("constr_viol", ctypes.c_void_p)]
 
 
 # every symbol declared in include/mpcracing.h (checked by tests/test_abi.py)

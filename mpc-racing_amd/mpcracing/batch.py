@@ -88,7 +88,7 @@ class BatchSolver:
                "S": torch.empty((N + 1, B), **f), "eC": torch.empty((N, B), **f), "eL": torch.empty((N, B), **f),
                "status": torch.empty(B, dtype=torch.int32, device=d),
                "iters": torch.empty(B, dtype=torch.int32, device=d),
-               "obj": torch.empty(B, **f), "kkt": torch.empty(B, **f)}
+               "obj": torch.empty(B, **f), "kkt": torch.empty(B, **f), "constr_viol": torch.empty(B, **f)}
         if duals:
             out["lam_g"] = torch.empty((13 * N + 9, B), **f)
         return out
@@ -116,7 +116,7 @@ class BatchSolver:
         o = abi.MROutputs(*[ptr(out.get(k)) for k in ("X", "U", "S", "eC", "eL", "status", "iters", "obj", "kkt",
                                                       "trace")], int(trace_instance),
                           int(tr.shape[0]) if tr is not None else 0, ptr(out.get("lam_g")),
-                          ptr(out.get("timeline")))
+                          ptr(out.get("timeline")), ptr(out.get("constr_viol")))
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
         self._check(self.lib.mr_solve_batch(self.h, B, ctypes.byref(inp), ctypes.byref(o),
                                             ctypes.c_void_p(st.cuda_stream)))

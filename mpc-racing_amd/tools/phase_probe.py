@@ -20,7 +20,7 @@ sys.path.insert(0, os.path.join(REPO, "mpc-racing_amd"))
 from mpcracing import workload as wl  # noqa: E402
 from mpcracing.batch import solver_for_config  # noqa: E402
 
-NAMES = ["eval", "riccati", "forward", "trial", "n_trials", "n_soc", "n_fact", "total"]
+NAMES = ["eval", "riccati", "forward", "trial", "n_trials", "n_soc_tries", "n_fact", "total"]
 
 
 def one(name, b, i, cap=520):
@@ -40,7 +40,8 @@ def one(name, b, i, cap=520):
     tr = out["trace"].cpu().numpy()
     it = int(out["iters"][0])
     row = dict(zip(NAMES, tr[-1].tolist()))
-    row.update(dict(zip(["fwd_seq", "fwd_par", "eval_stage", "eval_reduce", "fact_failed_cycles", "n_fact_failed"], tr[-2][:6].tolist())))
+    row.update(dict(zip(["fwd_seq", "fwd_par", "eval_stage", "eval_reduce", "fact_failed_cycles", "n_fact_failed",
+                        "soc_backward", "soc_forward"], tr[-2][:8].tolist())))
     row.update(instance=i, iters=it, status=int(out["status"][0]), wall_ms=1e3 * min(lat),
                cycles_per_iter=row["total"] / max(it, 1))
     return row
@@ -68,7 +69,7 @@ def main():
             it_i = int(o["iters"][i])
             row = dict(zip(NAMES, tr[-1].tolist()))
             row.update(dict(zip(["fwd_seq", "fwd_par", "eval_stage", "eval_reduce", "fact_failed_cycles",
-                                 "n_fact_failed"], tr[-2][:6].tolist())))
+                                 "n_fact_failed", "soc_backward", "soc_forward"], tr[-2][:8].tolist())))
             row.update(instance=i, iters=it_i, status=int(o["status"][i]), in_batch=True,
                        cycles_per_iter=row["total"] / max(it_i, 1))
             res[name].append(row)

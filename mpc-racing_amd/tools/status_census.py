@@ -1,0 +1,59 @@
+"""GPU census of a config's full per-GPU batch: IPOPT status histogram, iteration percentiles, the
+instances left at max_iter / status 3 / status 4, and the solve's wall time (the solver's default options:
+the reference's tol 1e-4 / acceptable_tol 1e-2 / acceptable_iter 15 unless overridden).
+
+Usage: python mpc-racing_amd/tools/status_census.py C3 C4 C5 [--tol 1e-8] [--out gpurun_out/census.json]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, ".."))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("configs", nargs="+")
+    ap.add_argument("--tol", type=float, default=None)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    import torch
+    from mpcracing import workload as wl
+    from mpcracing.batch import solver_for_config
+    recs = []
+    for name in a.configs:
+        cfg = wl.CONFIGS[name]
+        B = cfg["per_gpu"]
+        b = wl.make_batch(name, limit=B)
+        kw = {} if a.tol is None else dict(tol=a.tol)
+        s = solver_for_config(name, B, **kw)
+        ins, outs = s.to_device(b), s.alloc_outputs(B)
+        s.launch(ins, outs)  # warm-up (code object load)
+        torch.cuda.synchronize()
+        t0 = time.time()
+        s.launch(ins, outs)
+        torch.cuda.synchronize()
+        dt = time.time() - t0
+        st = outs["status"].cpu().numpy()
+        it = outs["iters"].cpu().numpy()
+        rec = {"config": name, "B": B, "precision": cfg["precision"], "tol": a.tol, "ms": round(dt * 1e3, 2),
+               "status": np.bincount(st, minlength=5).tolist(),
+               "iters_p50_p90_p99_max": [float(np.percentile(it, q)) for q in (50, 90, 99)] + [int(it.max())],
+               "max_iter_instances": np.where(st == 2)[0].tolist()[:64],
+               "status3_instances": np.where(st == 3)[0].tolist()[:64],
+               "status4_instances": np.where(st == 4)[0].tolist()[:64]}
+        print(json.dumps(rec), flush=True)
+        recs.append(rec)
+    if a.out:
+        with open(a.out, "w") as f:
+            for r in recs:
+                f.write(json.dumps(r) + "\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -54,13 +54,14 @@ def solve(cfg, batch, tyres=None, nthreads=8, trace_instance=-1, trace_cap=0, sc
                        _p(arr["runtime"]), _p(arr.get("u_init")))
     out = {"X": np.zeros((6, N + 1, B)), "U": np.zeros((2, N, B)), "S": np.zeros((N + 1, B)),
            "eC": np.zeros((N, B)), "eL": np.zeros((N, B)), "status": np.zeros(B, np.int32),
-           "iters": np.zeros(B, np.int32), "obj": np.zeros(B), "kkt": np.zeros(B)}
+           "iters": np.zeros(B, np.int32), "obj": np.zeros(B), "kkt": np.zeros(B), "constr_viol": np.zeros(B)}
     if trace_cap:
         out["trace"] = np.zeros((trace_cap, 8))
     if duals:
         out["lam_g"] = np.zeros((13 * N + 9, B))
     o = abi.MROutputs(*[_p(out.get(k)) for k in ("X", "U", "S", "eC", "eL", "status", "iters", "obj", "kkt",
-                                                 "trace")], trace_instance, trace_cap, _p(out.get("lam_g")), None)
+                                                 "trace")], trace_instance, trace_cap, _p(out.get("lam_g")), None,
+                      _p(out["constr_viol"]))
     if tyres is not None:
         (af, Fzf), (ar, Fzr) = tyres
         af = np.asarray(af, np.float64)

@@ -72,7 +72,10 @@ def test_horizon_extremes_match_host_build(N):
     o = {k: v.cpu().numpy() for k, v in s.solve(b).items()}
     h = ht.solve(ht.config(N, "kin", "fp64", tol=1e-10), b, nthreads=4)
     assert (o["status"] == h["status"]).all(), (o["status"], h["status"])
-    ok = o["status"] == 0
+    # at N = 63 the objective scaling is small enough that IPOPT's unscaled complementarity test fails at
+    # the mu floor: the solves end "acceptable" (status 1) at the same point on both builds
+    ok = o["status"] <= 1
+    assert ok.all()
     dU = np.abs(o["U"] - h["U"])[:, :, ok]
     dU[0, -1, :] = 0.0  # last throttle: fixed by the barrier only
     assert dU.max() < 1e-6 and np.abs(o["S"] - h["S"])[:, ok].max() < 1e-6
