@@ -130,7 +130,12 @@ struct CSF {
     RP = AZ + NZS, RN = RP + NI, RVP = RN + NI, RVN = RVP + NI, RDP = RVN + NI, RDN = RDP + NI, RDVP = RDN + NI,
     RDVN = RDVP + NI, RY = RDVN + NI, RDY = RY + NI, RZ = RDY + NI,
     CP = RZ + NZS, CN = CP + 6, CVP = CN + 6, CVN = CVP + 6, CDP = CVN + 6, CDN = CDP + 6, CDVP = CDN + 6,
-    CDVN = CDVP + 6, CSW = CDVN + 6, CGW0 = CSW + 6, CGW1 = CGW0 + 6, NF = CGW1 + 6
+    CDVN = CDVP + 6, CSW = CDVN + 6, CGW0 = CSW + 6, CGW1 = CGW0 + 6,
+    // second-order corrections in closed-loop form: Acl = A + B K (row-major), P_{k+1} c_k, the
+    // costate recursion's constant b and the state recursion's constant e
+    SACL = CGW1 + 6, SPC = SACL + NX * NX, SB = SPC + NX, SE = SB + NX,
+    SJUNK = SE + NX,  // discard slot of the chains' lanes without a component
+    NF = SJUNK + 1
   };
 };
 // The dynamics rows' multipliers nu (and their watchdog snapshot) in fp64 whatever the solve precision,
@@ -1858,15 +1863,19 @@ struct WaveSolver {
     }
     wsync(w);
   }
-  // the SOC's costate vector and feed-forward: stage gradients with the rows' r_soc (lane = stage), then
-  // pc = P_{k+1} c_k + p_{k+1}, r = g_u + B^T pc, k = -Q_uu^-1 r, p_k = g_x + A^T pc + K^T r (wave-uniform)
+  // the SOC's costate vector and feed-forward on the stored factorisation, in closed-loop form: with
+  // Acl_k = A_k + B_k K_k and pc = pv_{k+1} + P_{k+1} c_k,
+  //   pv_k = g_x + A^T pc + K^T (B^T pc + g_u) = Acl_k^T pv_{k+1} + b_k,  b_k = Acl_k^T P_{k+1} c_k + g_x + K_k^T g_u,
+  //   k_k  = -Q_uu^-1 (B^T pc + g_u).
+  // Everything but the chain pv_{k+1} -> pv_k is stage-parallel (lane = stage); the chain runs on lanes
+  // 0..10 (lane i: component i, the others' by v_readlane), 11 multiply-adds per stage.
   MR_SWEEP void soc_backward() {
     MR_UNIFORM_P();
     MR_ASSUME_LDS_STATE();
     const T mu = this->mu, dl = cw()->delta_it;
     const int N = wu(w, this->N);
+    const int k = ln;
     if (own()) {
-      const int k = ln;
       const MR_GLOBAL T* Rk = R(k);
       T g[NZ];
       for (int i = 0; i < NZ; ++i) g[i] = Rk[RCF::G0 + i] + mu * Rk[RCF::G1 + i] + dl * Rk[RCF::GD + i];
@@ -1896,27 +1905,62 @@ struct WaveSolver {
         }
       }
       for (int i = 0; i < NZ; ++i) Cf(CSF::SG + i) = g[i];
+      if (k < N) {
+        const MR_GLOBAL T* Rn = R(k + 1);
+        T J[48], Kk[NU * NX], c[NX], pcv[NX];
+        for (int i = 0; i < 48; ++i) J[i] = Rk[RCF::J + i];
+        for (int i = 0; i < NU * NX; ++i) Kk[i] = Rk[RCF::K + i];
+        for (int i = 0; i < NX; ++i) c[i] = Cf(CSF::SC + i);
+        for (int i = 0; i < NX; ++i) {
+          T v = T(0);
+          for (int l = 0; l < NX; ++l) v += Rn[RCF::P + pidx(i, l)] * c[l];
+          pcv[i] = v;
+          Cf(CSF::SPC + i) = v;
+        }
+        T b[NX];
+        for (int j = 0; j < NX; ++j) b[j] = g[j] + Kk[0 * NX + j] * g[NX] + Kk[1 * NX + j] * g[NX + 1] + Kk[2 * NX + j] * g[NX + 2];
+        for (int j = 0; j < NX; ++j) {  // column j of Acl
+          T ej[NX], kj[NU], ta[NX], tb[NX];
+          for (int i = 0; i < NX; ++i) ej[i] = i == j ? T(1) : T(0);
+          for (int a = 0; a < NU; ++a) kj[a] = Kk[a * NX + j];
+          apply_A(J, k, ej, ta);
+          apply_B(J, k, kj, tb);
+          for (int i = 0; i < NX; ++i) {
+            const T v = ta[i] + tb[i];
+            Cf(CSF::SACL + i * NX + j) = v;
+            b[j] += v * pcv[i];
+          }
+        }
+        for (int j = 0; j < NX; ++j) Cf(CSF::SB + j) = b[j];
+      }
     }
     wsync(w);
-    const MR_GLOBAL T* cb = rc + (int64_t)RC_STRIDE * WL;
-    T pv[NX];
-    for (int i = 0; i < NX; ++i) pv[i] = cb[(CSF::SG + i) * WL + N];
-    if (ln == N)
-      for (int i = 0; i < NX; ++i) Cf(CSF::SPV + i) = pv[i];
-    for (int k = N - 1; k >= 0; --k) {
-      const MR_GLOBAL T* Rk = R(k);
-      const MR_GLOBAL T* Rn = R(k + 1);
-      T J[48];
-      for (int i = 0; i < 48; ++i) J[i] = Rk[RCF::J + i];
-      T pc[NX];
-      for (int i = 0; i < NX; ++i) {
-        T acc = pv[i];
-        for (int l = 0; l < NX; ++l) acc += Rn[RCF::P + pidx(i, l)] * cb[(CSF::SC + l) * WL + k];
-        pc[i] = acc;
+    {  // the chain: lane i < NX carries pv[i]; stores through a buffer resource (no ordering of the loads)
+      const MR_GLOBAL T* cb = rc + (int64_t)RC_STRIDE * WL;
+      const WBuf<T> wb(rc + (int64_t)RC_STRIDE * WL, (unsigned)CSF::NF * WL);
+      const bool row = ln < NX;
+      const int li = row ? ln : 0;
+      T pv = cb[(CSF::SG + li) * WL + N];
+      const unsigned junk = (unsigned)(CSF::SJUNK * WL + ln);
+      wb.st(pv, 0u, row ? (unsigned)((CSF::SPV + li) * WL + N) : junk);
+      for (int kk = N - 1; kk >= 0; --kk) {
+        T acl[NX];
+        for (int j = 0; j < NX; ++j) acl[j] = cb[(CSF::SACL + j * NX + li) * WL + kk];
+        T v = cb[(CSF::SB + li) * WL + kk];
+        for (int j = 0; j < NX; ++j) v += acl[j] * wbcast(w, pv, j);
+        pv = v;
+        wb.st(pv, 0u, row ? (unsigned)((CSF::SPV + li) * WL + kk) : junk);
       }
-      T r[NU];
+    }
+    wsync(w);
+    if (own() && k < N) {  // the feed-forward, stage-parallel
+      const MR_GLOBAL T* Rk = R(k);
+      const MR_GLOBAL T* cb = rc + (int64_t)RC_STRIDE * WL;
+      T J[48], pc[NX], r[NU];
+      for (int i = 0; i < 48; ++i) J[i] = Rk[RCF::J + i];
+      for (int i = 0; i < NX; ++i) pc[i] = cb[(CSF::SPV + i) * WL + k + 1] + Cf(CSF::SPC + i);
       apply_Bt(J, k, pc, r);
-      for (int a = 0; a < NU; ++a) r[a] += cb[(CSF::SG + NX + a) * WL + k];
+      for (int a = 0; a < NU; ++a) r[a] += Cf(CSF::SG + NX + a);
       // k = -Q_uu^-1 r with Q_uu = L L^T (L10, L20, L21, reciprocal pivots from the Riccati sweep)
       const T L1 = Rk[RCF::LQ + 0], L3 = Rk[RCF::LQ + 1], L4 = Rk[RCF::LQ + 2];
       const T iv[3] = {Rk[RCF::LQ + 3], Rk[RCF::LQ + 4], Rk[RCF::LQ + 5]};
@@ -1924,65 +1968,66 @@ struct WaveSolver {
       T kf[NU] = {-r[0], -r[1], -r[2]};
       lsolve3r(Lf, iv, kf);
       ltsolve3r(Lf, iv, kf);
-      T at[NX];
-      apply_At(J, k, pc, at);
-      for (int i = 0; i < NX; ++i) {
-        T v = cb[(CSF::SG + i) * WL + k] + at[i];
-        for (int a = 0; a < NU; ++a) v += Rk[RCF::K + a * NX + i] * r[a];
-        pv[i] = v;
-      }
-      if (ln == k) {
-        for (int a = 0; a < NU; ++a) Cf(CSF::SK0 + a) = kf[a];
-        for (int i = 0; i < NX; ++i) Cf(CSF::SPV + i) = pv[i];
-      }
+      for (int a = 0; a < NU; ++a) Cf(CSF::SK0 + a) = kf[a];
     }
     wsync(w);
   }
-  // the SOC direction (mr_solver.h Solver::forward with soc set): SDZ, SDS, SDLAM, SDY, SDNU
+  // the SOC direction (mr_solver.h Solver::forward with soc set): SDZ, SDS, SDLAM, SDY, SDNU.
+  // dx_{k+1} = Acl_k dx_k + e_k with e_k = B_k k_k + c_k: e stage-parallel, the chain on lanes 0..10
+  // (dx_k to SDZ[0..10] of stage k), then du_k = k_k + K_k dx_k and the costate step
+  // dnu_k = pv_k + P_k dx_k stage-parallel
   MR_SWEEP void forward_soc(T& ap, T& ad) {
     MR_UNIFORM_P();
     MR_ASSUME_LDS_STATE();
     const T tau = mr_max(T(0.99), T(1) - mu);
     const int N = wu(w, this->N);
     const MR_GLOBAL T* cb = rc + (int64_t)RC_STRIDE * WL;
-    T dx[NX], mydz[NZS];
-    for (int i = 0; i < NX; ++i) dx[i] = T(0);
-    for (int i = 0; i < NZS; ++i) mydz[i] = T(0);
-    if (ln == 0 && !MR_KKT_RESTATED)  // the initial-state rows' multiplier step: stage 0's costate
-      for (int i = 0; i < NX; ++i) Cf(CSF::SDNU + i) = Cf(CSF::SPV + i);
-    for (int k = 0; k <= N; ++k) {
+    if (own() && ln < N) {
+      const int k = ln;
       const MR_GLOBAL T* Rk = R(k);
-      T du[NU] = {T(0), T(0), T(0)};
-      if (k < N)
-        for (int a = 0; a < NU; ++a) {
-          T v = cb[(CSF::SK0 + a) * WL + k];
-          for (int j = 0; j < NX; ++j) v += Rk[RCF::K + a * NX + j] * dx[j];
-          du[a] = v;
-        }
-      if (ln == k) {
-        for (int i = 0; i < NX; ++i) mydz[i] = dx[i];
-        for (int a = 0; a < NU; ++a) mydz[NX + a] = du[a];
-      }
-      if (k == N) break;
-      T J[48], t[NX], tb[NX];
+      T J[48], kf[NU], tb[NX];
       for (int i = 0; i < 48; ++i) J[i] = Rk[RCF::J + i];
-      apply_A(J, k, dx, t);
-      apply_B(J, k, du, tb);
-      for (int i = 0; i < NX; ++i) dx[i] = t[i] + tb[i] + cb[(CSF::SC + i) * WL + k];
-      if (ln == k + 1) {  // the costate (multiplier) step of x_{k+1}'s rows
-        const MR_GLOBAL T* Rn = R(k + 1);
-        for (int i = 0; i < NX; ++i) {
-          T v = Cf(CSF::SPV + i);
-          for (int l = 0; l < NX; ++l) v += Rn[RCF::P + pidx(i, l)] * dx[l];
-          Cf(CSF::SDNU + i) = v;
-        }
+      for (int a = 0; a < NU; ++a) kf[a] = Cf(CSF::SK0 + a);
+      apply_B(J, k, kf, tb);
+      for (int i = 0; i < NX; ++i) Cf(CSF::SE + i) = tb[i] + Cf(CSF::SC + i);
+    }
+    wsync(w);
+    {
+      const WBuf<T> wb(rc + (int64_t)RC_STRIDE * WL, (unsigned)CSF::NF * WL);
+      const bool row = ln < NX;
+      const int li = row ? ln : 0;
+      const unsigned junk = (unsigned)(CSF::SJUNK * WL + ln);
+      T dx = T(0);
+      wb.st(dx, 0u, row ? (unsigned)((CSF::SDZ + li) * WL + 0) : junk);
+      for (int kk = 0; kk < N; ++kk) {
+        T acl[NX];
+        for (int j = 0; j < NX; ++j) acl[j] = cb[(CSF::SACL + li * NX + j) * WL + kk];
+        T v = cb[(CSF::SE + li) * WL + kk];
+        for (int j = 0; j < NX; ++j) v += acl[j] * wbcast(w, dx, j);
+        dx = v;
+        wb.st(dx, 0u, row ? (unsigned)((CSF::SDZ + li) * WL + kk + 1) : junk);
       }
     }
+    wsync(w);
     T ap_l = T(1), ad_l = T(1), g_l = T(0);
     if (own()) {
       const int k = ln;
+      const MR_GLOBAL T* Rk = R(k);
       T dz[NZS];
-      for (int i = 0; i < NZS; ++i) dz[i] = mydz[i];
+      for (int i = 0; i < NZS; ++i) dz[i] = T(0);
+      for (int i = 0; i < NX; ++i) dz[i] = Cf(CSF::SDZ + i);
+      if (k < N)
+        for (int a = 0; a < NU; ++a) {
+          T v = Cf(CSF::SK0 + a);
+          for (int j = 0; j < NX; ++j) v += Rk[RCF::K + a * NX + j] * dz[j];
+          dz[NX + a] = v;
+        }
+      if (k > 0 || !MR_KKT_RESTATED)  // the costate (multiplier) step of x_k's rows (k = 0: the initial-state rows')
+        for (int i = 0; i < NX; ++i) {
+          T v = Cf(CSF::SPV + i);
+          for (int l = 0; l < NX; ++l) v += Rk[RCF::P + pidx(i, l)] * dz[l];
+          Cf(CSF::SDNU + i) = v;
+        }
       T z[NZS];
       load_z(cur, z);
       Err<T> e;

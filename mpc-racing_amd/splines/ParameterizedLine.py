@@ -9,8 +9,8 @@ callers such as ``TrackSegments``).  Query methods take scalars (scalar results)
 
 Differences from the reference, both documented in DESIGN.md: ``projection_global`` (:99-105,
 scipy's unseeded ``dual_annealing``) is a deterministic search -- the local bounded Brent on every
-5 m window, best distance wins; ``x_as_coeffs`` / ``y_as_coeffs`` support the agent's quartic
-(``deg = 4``) only.
+5 m window, best distance wins; ``x_as_coeffs`` / ``y_as_coeffs`` take degrees 0..10 on the device
+(``mr_track_polyfit_deg``; the agent uses the quartic), the reference's ``np.polyfit`` any degree.
 """
 import numpy as np
 
