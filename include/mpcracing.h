@@ -92,7 +92,10 @@ typedef struct mr_config {
      corner of the model); tier 1 = the rest outside 16.5 < v < 39; tier 2 = the others (a cold-start
      guess from the model's nonsmooth / stiff regions, for batches without history);
      2 = longest-expected-first by mr_inputs.order_hint (e.g. the previous MPC tick's iters of the same
-     vehicles: LPT scheduling with a distribution-agnostic estimate; instance order when the hint is NULL) */
+     vehicles: LPT scheduling with a distribution-agnostic estimate); without a hint, the handle's own
+     previous solve of the same batch size (its iters, kept on the device and read in stream order: calls
+     on different streams must be ordered by the caller), else instance order; a uniform hint (all equal)
+     gives instance order */
   int32_t dispatch_order;
 } mr_config;
 

@@ -26,6 +26,8 @@ struct mr_handle {
   void* ws;
   size_t ws_bytes;
   int* order;  // [max_batch] workgroup -> instance (mr_order_kernel)
+  int32_t* last_iters;  // [max_batch] the previous solve's iterations (dispatch_order 2's default hint)
+  int last_B;           // batch size of that solve (0: none yet)
   TyreCoef<double> tf, tr;
   int have_tyres;
 };
@@ -193,22 +195,19 @@ __global__ __launch_bounds__(kOrderThreads) void mr_order_kernel(const double* s
 // the previous MPC tick's iteration counts.  One workgroup: bucket histogram (hint clamped to
 // 0..kHintBuckets-1) in LDS, a scan from the largest bucket down, then an atomic scatter (the order within
 // a bucket is arbitrary; results do not depend on the order).  A hint that says nothing (every instance in
-// one bucket, e.g. all zero on a first tick) falls back to dispatch_order 1's distribution-agnostic tiers.
+// one bucket, e.g. all zero) gives instance order: no model-specific guess.
 constexpr int kHintBuckets = kOrderThreads;
 __device__ __forceinline__ int hint_bucket(int h) { return h < 0 ? 0 : (h >= kHintBuckets ? kHintBuckets - 1 : h); }
-__global__ __launch_bounds__(kOrderThreads) void mr_order_hint_kernel(const int32_t* hint, const double* state0,
-                                                                      int B, int* order) {
+__global__ __launch_bounds__(kOrderThreads) void mr_order_hint_kernel(const int32_t* hint, int B, int* order) {
   __shared__ int cnt[kHintBuckets];
   __shared__ int scan[kOrderThreads];
-  __shared__ int tot[2];
   const int t = threadIdx.x;
   cnt[t] = 0;
   __syncthreads();
   for (int i = t; i < B; i += kOrderThreads) atomicAdd(&cnt[hint_bucket(hint[i])], 1);
   __syncthreads();
-  if (cnt[hint_bucket(hint[0])] == B) {  // uniform hint: block-uniform branch
-    __syncthreads();
-    order_tiers(state0, B, order, scan, tot);
+  if (cnt[hint_bucket(hint[0])] == B) {  // uniform hint (block-uniform branch): instance order
+    for (int i = t; i < B; i += kOrderThreads) order[i] = i;
     return;
   }
   const int r = kHintBuckets - 1 - t;  // thread t scans bucket r: the largest bucket first
@@ -246,18 +245,22 @@ static int launch(mr_handle* h, int B, const mr_inputs* in, mr_outputs* out, hip
     HIP_TRY(hipGetLastError());
     order = h->order;
   } else if (h->cfg.dispatch_order == 2 && B > 1) {
-    // without a hint: dispatch_order 1's tiers
-    if (in->order_hint)
-      hipLaunchKernelGGL(mr_order_hint_kernel, dim3(1), dim3(kOrderThreads), 0, st, in->order_hint, in->state0, B,
-                         h->order);
-    else
-      hipLaunchKernelGGL(mr_order_kernel, dim3(1), dim3(kOrderThreads), 0, st, in->state0, B, h->order);
-    HIP_TRY(hipGetLastError());
-    order = h->order;
+    // the caller's hint, else the handle's previous solve of the same batch size (the closed loop's
+    // previous tick), else instance order -- no model-specific guess
+    const int32_t* hint = in->order_hint ? in->order_hint : (h->last_B == B ? h->last_iters : nullptr);
+    if (hint) {
+      hipLaunchKernelGGL(mr_order_hint_kernel, dim3(1), dim3(kOrderThreads), 0, st, hint, B, h->order);
+      HIP_TRY(hipGetLastError());
+      order = h->order;
+    }
   }
   hipLaunchKernelGGL((mr_wave_kernel<T, MODEL>), dim3(B), dim3(WL), 0, st, (const ProbParams<T>*)h->params_dev, *in,
                      *out, B, (T*)h->ws, order);
   HIP_TRY(hipGetLastError());
+  if (h->cfg.dispatch_order == 2) {  // this solve's iterations: the next call's default hint
+    HIP_TRY(hipMemcpyAsync(h->last_iters, out->iters, sizeof(int32_t) * (size_t)B, hipMemcpyDeviceToDevice, st));
+    h->last_B = B;
+  }
   return MR_OK;
 }
 
@@ -502,12 +505,16 @@ int mr_create(mr_handle** out, const mr_config* cfg) {
   memset(&h->tr, 0, sizeof(h->tr));
   h->ws_bytes = ws_bytes_per_instance(*cfg) * (size_t)cfg->max_batch;
   h->order = nullptr;
+  h->last_iters = nullptr;
+  h->last_B = 0;
   hipError_t e = hipMalloc(&h->ws, h->ws_bytes);
   if (e == hipSuccess) e = hipMalloc((void**)&h->order, sizeof(int) * (size_t)cfg->max_batch);
+  if (e == hipSuccess) e = hipMalloc((void**)&h->last_iters, sizeof(int32_t) * (size_t)cfg->max_batch);
   if (e == hipSuccess) e = hipMalloc(&h->params_dev, sizeof(ProbParams<double>));
   if (e != hipSuccess) {
     if (h->ws) (void)hipFree(h->ws);
     if (h->order) (void)hipFree(h->order);
+    if (h->last_iters) (void)hipFree(h->last_iters);
     delete h;
     return fail(MR_ERR_HIP, std::string("workspace hipMalloc: ") + hipGetErrorString(e));
   }
@@ -526,6 +533,7 @@ int mr_destroy(mr_handle* h) {
   if (!h) return MR_OK;
   if (h->ws) (void)hipFree(h->ws);
   if (h->order) (void)hipFree(h->order);
+  if (h->last_iters) (void)hipFree(h->last_iters);
   if (h->params_dev) (void)hipFree(h->params_dev);
   delete h;
   return MR_OK;

@@ -1943,10 +1943,18 @@ struct WaveSolver {
       T pv = cb[(CSF::SG + li) * WL + N];
       const unsigned junk = (unsigned)(CSF::SJUNK * WL + ln);
       wb.st(pv, 0u, row ? (unsigned)((CSF::SPV + li) * WL + N) : junk);
+      // operands of the next stage loaded one stage ahead (the chain is latency-bound)
+      T acl_n[NX], b_n;
+      auto ld = [&](int kk, T* acl, T& bb) {
+        for (int j = 0; j < NX; ++j) acl[j] = cb[(CSF::SACL + j * NX + li) * WL + kk];
+        bb = cb[(CSF::SB + li) * WL + kk];
+      };
+      if (N > 0) ld(N - 1, acl_n, b_n);
       for (int kk = N - 1; kk >= 0; --kk) {
         T acl[NX];
-        for (int j = 0; j < NX; ++j) acl[j] = cb[(CSF::SACL + j * NX + li) * WL + kk];
-        T v = cb[(CSF::SB + li) * WL + kk];
+        for (int j = 0; j < NX; ++j) acl[j] = acl_n[j];
+        T v = b_n;
+        if (kk > 0) ld(kk - 1, acl_n, b_n);
         for (int j = 0; j < NX; ++j) v += acl[j] * wbcast(w, pv, j);
         pv = v;
         wb.st(pv, 0u, row ? (unsigned)((CSF::SPV + li) * WL + kk) : junk);
@@ -1999,10 +2007,17 @@ struct WaveSolver {
       const unsigned junk = (unsigned)(CSF::SJUNK * WL + ln);
       T dx = T(0);
       wb.st(dx, 0u, row ? (unsigned)((CSF::SDZ + li) * WL + 0) : junk);
+      T acl_n[NX], e_n;  // operands of the next stage loaded one stage ahead
+      auto ld = [&](int kk, T* acl, T& ee) {
+        for (int j = 0; j < NX; ++j) acl[j] = cb[(CSF::SACL + li * NX + j) * WL + kk];
+        ee = cb[(CSF::SE + li) * WL + kk];
+      };
+      if (N > 0) ld(0, acl_n, e_n);
       for (int kk = 0; kk < N; ++kk) {
         T acl[NX];
-        for (int j = 0; j < NX; ++j) acl[j] = cb[(CSF::SACL + li * NX + j) * WL + kk];
-        T v = cb[(CSF::SE + li) * WL + kk];
+        for (int j = 0; j < NX; ++j) acl[j] = acl_n[j];
+        T v = e_n;
+        if (kk + 1 < N) ld(kk + 1, acl_n, e_n);
         for (int j = 0; j < NX; ++j) v += acl[j] * wbcast(w, dx, j);
         dx = v;
         wb.st(dx, 0u, row ? (unsigned)((CSF::SDZ + li) * WL + kk + 1) : junk);

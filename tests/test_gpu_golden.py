@@ -66,3 +66,43 @@ def test_gpu_fp64_matches_oracle_solutions(name):
         (same if (d < 1e-6 and rel < 1e-8) else other).append((int(i), float(d), float(rel)))
     print(f"{name}: {len(same)} of {int(ok.sum())} oracle-solved instances match to 1e-6; other local minima: {other}")
     assert len(other) <= max(1, int(0.1 * ok.sum())), other
+
+
+@pytest.mark.parametrize("name", ["C4", "C5"])
+def test_gpu_fp32_vs_oracle_solutions(name):
+    """fp32 (the benchmarked precision) on the fixture's inputs, with the reference's IPOPT options
+    (MPC.py:152-161), against the oracle's exact fp64 solutions -- the DESIGN.md §4 bar, anchored on the
+    committed oracle points instead of a GPU fp64 solve: where fp32 and an fp64 solve with the same
+    options both return a point from the mu floor (converged, or stopped almost feasible), the fp32
+    control error to the oracle is distributed like the
+    fp64 one (median within 1.5x + 1e-4, largest within 3x + 1e-3) and so is the objective gap (median
+    and largest within 1.5x / 3x + 1e-6); the IPOPT outcome agrees on >= 85 % of instances, and a status-3
+    stop of either precision is an almost-feasible point (constraint violation <= 1e-4)."""
+    g = _fixture(name)
+    cfg = wl.CONFIGS[name]
+    b = wl.make_batch(name, limit=g["status"].size)
+    tyres = wl.tyre_coeffs(cfg["tyres"]) if cfg["tyres"] else None
+    n = b["s0"].shape[0]
+    mk = lambda prec: BatchSolver(cfg["N"], cfg["model"], prec, max_batch=n, tyres=tyres, tol=1e-4,  # noqa: E731
+                                  acceptable_tol=1e-2, acceptable_iter=15)
+    o32 = {k: v.cpu().numpy() for k, v in mk("fp32").solve(b).items()}
+    o64 = {k: v.cpu().numpy() for k, v in mk("fp64").solve(b).items()}
+    assert (o32["status"] == o64["status"]).mean() >= 0.85, (o32["status"], o64["status"])
+    for o in (o32, o64):
+        s3 = o["status"] == 3
+        assert (o["constr_viol"][s3] <= 1e-4).mean() >= 0.9 if s3.any() else True, o["constr_viol"][s3]
+    # compared where the oracle converged and both returned a point from the mu floor: converged, or the
+    # status-3 stop at an almost-feasible point (C5: df ~ 1e-4 makes that every instance's outcome)
+    fl = lambda o: (o["status"] <= 1) | ((o["status"] == 3) & (o["constr_viol"] <= 1e-4))  # noqa: E731
+    ok = (g["status"] == 0) & fl(o32) & fl(o64)
+    assert ok.sum() >= 8, (g["status"], o32["status"], o64["status"])
+    d32 = np.abs(g["U"] - o32["U"])[:, :-1, ok].max(axis=(0, 1))
+    d64 = np.abs(g["U"] - o64["U"])[:, :-1, ok].max(axis=(0, 1))
+    assert np.median(d32) <= 1.5 * np.median(d64) + 1e-4, (d32, d64)
+    assert d32.max() <= 3.0 * d64.max() + 1e-3, (d32, d64)
+    loc = lambda o: o["obj"][ok] + 300.0 * b["s0"][ok]  # noqa: E731  (-lambda_s s0 removed)
+    gl = g["obj"][ok] + 300.0 * b["s0"][ok]
+    g32, g64 = (loc(o32) - gl) / np.abs(gl), (loc(o64) - gl) / np.abs(gl)
+    assert np.median(g32) <= 1.5 * np.median(g64) + 1e-6 and g32.max() <= 3.0 * g64.max() + 1e-6, (g32, g64)
+    print(f"{name}: fp32 statuses {np.bincount(o32['status'], minlength=5)}, compared {int(ok.sum())}; "
+          f"median |dU| fp32 {np.median(d32):.2e} fp64 {np.median(d64):.2e}")
