@@ -681,6 +681,9 @@ struct SolveOut {
   double viol;  // IPOPT's unscaled constraint violation of the returned point (max-norm, mr_outputs.constr_viol)
 };
 
+#ifndef MR_F32_STALL
+#define MR_F32_STALL 15  // fp32 stall exit at the mu floor (iterations; 0 = off), see Solver::solve
+#endif
 #ifndef MR_FMAX
 #define MR_FMAX 32  // filter entries kept (IPOPT: unbounded; the oracle's longest filter on the audits is 32)
 #endif
@@ -2150,7 +2153,7 @@ struct Solver {
     const T mu_min = mr_max(T(1e-11), mr_min(P.tol, T(IP_COMPL_INF_TOL)) / (kappa_eps + T(1)));
     SolveOut out{2, 0, 0.0, 0.0, 0.0};
     T mu_prev = mu;
-    int acc_count = 0;
+    int acc_count = 0, stall = 0;
     // IPOPT's filter reset heuristic (filter_reset_trigger = 5, max_filter_resets = 5): after this many
     // successive iterations whose line search had a trial point rejected by the filter, clear it
     int filt_rej_iters = 0, filt_resets = 0;
@@ -2182,6 +2185,24 @@ struct Solver {
         if (P.acc_iter > 0) {
           acc_count = acceptable(kkt) ? acc_count + 1 : 0;
           if (acc_count >= P.acc_iter) { out.status = 1; break; }
+        }
+        // fp32 only: at the mu floor, feasible to IPOPT's constr_viol_tol, without meeting
+        // the convergence tests for MR_F32_STALL iterations -> the fp64 solve's outcome there (the line
+        // search fails at the floor: the stored acceptable point or status 3).  In fp32 the constraint
+        // violation and phi carry rounding noise well above that line search's resolution, so trial
+        // points keep being accepted and the solve would run to max_iter instead.
+        if (sizeof(T) == 4 && MR_F32_STALL > 0) {
+          stall = (mu <= mu_min && mr_max(pr_eq, viol_max) <= T(IP_CONSTR_VIOL_TOL)) ? stall + 1 : 0;
+          if (stall >= MR_F32_STALL) {
+            if (have_acc) {
+              acc_restore();
+              out.status = 1;
+              out.kkt = acc_kkt; out.obj = acc_obj; out.viol = acc_viol;
+            } else {
+              out.status = 3;
+            }
+            break;
+          }
         }
       }
       if (it >= P.max_iter) { out.status = 2; break; }
@@ -2337,7 +2358,8 @@ struct Solver {
         // the current point acceptable -> "acceptable point reached"; almost feasible (theta <= 1e-2 tol)
         // -> the stored acceptable point, or restoration failed; otherwise the restoration phase
         if (acceptable(kkt)) { out.status = 1; break; }
-        if (theta <= T(1e-2) * P.tol) {
+        if (theta <= T(1e-2) * P.tol ||
+            (sizeof(T) == 4 && mr_max(pr_eq, viol_max) <= T(IP_CONSTR_VIOL_TOL))) {  // fp32: feasible at its resolution
           if (have_acc) {
             acc_restore();
             out.status = 1;

@@ -131,10 +131,7 @@ struct CSF {
     RDVN = RDVP + NI, RY = RDVN + NI, RDY = RY + NI, RZ = RDY + NI,
     CP = RZ + NZS, CN = CP + 6, CVP = CN + 6, CVN = CVP + 6, CDP = CVN + 6, CDN = CDP + 6, CDVP = CDN + 6,
     CDVN = CDVP + 6, CSW = CDVN + 6, CGW0 = CSW + 6, CGW1 = CGW0 + 6,
-    // second-order corrections in closed-loop form: Acl = A + B K (row-major), P_{k+1} c_k, the
-    // costate recursion's constant b and the state recursion's constant e
-    SACL = CGW1 + 6, SPC = SACL + NX * NX, SB = SPC + NX, SE = SB + NX,
-    SJUNK = SE + NX,  // discard slot of the chains' lanes without a component
+    SJUNK = CGW1 + 6,  // discard slot of the SOC chains' lanes without a component
     NF = SJUNK + 1
   };
 };
@@ -1863,19 +1860,19 @@ struct WaveSolver {
     }
     wsync(w);
   }
-  // the SOC's costate vector and feed-forward on the stored factorisation, in closed-loop form: with
-  // Acl_k = A_k + B_k K_k and pc = pv_{k+1} + P_{k+1} c_k,
-  //   pv_k = g_x + A^T pc + K^T (B^T pc + g_u) = Acl_k^T pv_{k+1} + b_k,  b_k = Acl_k^T P_{k+1} c_k + g_x + K_k^T g_u,
-  //   k_k  = -Q_uu^-1 (B^T pc + g_u).
-  // Everything but the chain pv_{k+1} -> pv_k is stage-parallel (lane = stage); the chain runs on lanes
-  // 0..10 (lane i: component i, the others' by v_readlane), 11 multiply-adds per stage.
+  // The SOC's costate vector and feed-forward on the stored factorisation:
+  //   pc = pv_{k+1} + P_{k+1} c_k,  r = B^T pc + g_u,  k_k = -Q_uu^-1 r,  pv_k = g_x + A^T pc + K^T r.
+  // The stage gradients (with the rows' r_soc) are stage-parallel (lane = stage); the recursion runs on
+  // lanes 0..10 (lane i: component i of pc / pv, the others' by v_readlane), every lane gathering its
+  // row of P_{k+1}, its column of A_k and K_k from the stage's record (a few cache lines per stage) and
+  // the shared terms (B's J columns, Q_uu's factor, c_k, g_u) as uniform loads, one stage ahead.
   MR_SWEEP void soc_backward() {
     MR_UNIFORM_P();
     MR_ASSUME_LDS_STATE();
     const T mu = this->mu, dl = cw()->delta_it;
     const int N = wu(w, this->N);
-    const int k = ln;
     if (own()) {
+      const int k = ln;
       const MR_GLOBAL T* Rk = R(k);
       T g[NZ];
       for (int i = 0; i < NZ; ++i) g[i] = Rk[RCF::G0 + i] + mu * Rk[RCF::G1 + i] + dl * Rk[RCF::GD + i];
@@ -1905,122 +1902,128 @@ struct WaveSolver {
         }
       }
       for (int i = 0; i < NZ; ++i) Cf(CSF::SG + i) = g[i];
-      if (k < N) {
-        const MR_GLOBAL T* Rn = R(k + 1);
-        T J[48], Kk[NU * NX], c[NX], pcv[NX];
-        for (int i = 0; i < 48; ++i) J[i] = Rk[RCF::J + i];
-        for (int i = 0; i < NU * NX; ++i) Kk[i] = Rk[RCF::K + i];
-        for (int i = 0; i < NX; ++i) c[i] = Cf(CSF::SC + i);
-        for (int i = 0; i < NX; ++i) {
-          T v = T(0);
-          for (int l = 0; l < NX; ++l) v += Rn[RCF::P + pidx(i, l)] * c[l];
-          pcv[i] = v;
-          Cf(CSF::SPC + i) = v;
-        }
-        T b[NX];
-        for (int j = 0; j < NX; ++j) b[j] = g[j] + Kk[0 * NX + j] * g[NX] + Kk[1 * NX + j] * g[NX + 1] + Kk[2 * NX + j] * g[NX + 2];
-        for (int j = 0; j < NX; ++j) {  // column j of Acl
-          T ej[NX], kj[NU], ta[NX], tb[NX];
-          for (int i = 0; i < NX; ++i) ej[i] = i == j ? T(1) : T(0);
-          for (int a = 0; a < NU; ++a) kj[a] = Kk[a * NX + j];
-          apply_A(J, k, ej, ta);
-          apply_B(J, k, kj, tb);
-          for (int i = 0; i < NX; ++i) {
-            const T v = ta[i] + tb[i];
-            Cf(CSF::SACL + i * NX + j) = v;
-            b[j] += v * pcv[i];
-          }
-        }
-        for (int j = 0; j < NX; ++j) Cf(CSF::SB + j) = b[j];
-      }
     }
     wsync(w);
-    {  // the chain: lane i < NX carries pv[i]; stores through a buffer resource (no ordering of the loads)
-      const MR_GLOBAL T* cb = rc + (int64_t)RC_STRIDE * WL;
-      const WBuf<T> wb(rc + (int64_t)RC_STRIDE * WL, (unsigned)CSF::NF * WL);
-      const bool row = ln < NX;
-      const int li = row ? ln : 0;
-      T pv = cb[(CSF::SG + li) * WL + N];
-      const unsigned junk = (unsigned)(CSF::SJUNK * WL + ln);
-      wb.st(pv, 0u, row ? (unsigned)((CSF::SPV + li) * WL + N) : junk);
-      // operands of the next stage loaded one stage ahead (the chain is latency-bound)
-      T acl_n[NX], b_n;
-      auto ld = [&](int kk, T* acl, T& bb) {
-        for (int j = 0; j < NX; ++j) acl[j] = cb[(CSF::SACL + j * NX + li) * WL + kk];
-        bb = cb[(CSF::SB + li) * WL + kk];
-      };
-      if (N > 0) ld(N - 1, acl_n, b_n);
-      for (int kk = N - 1; kk >= 0; --kk) {
-        T acl[NX];
-        for (int j = 0; j < NX; ++j) acl[j] = acl_n[j];
-        T v = b_n;
-        if (kk > 0) ld(kk - 1, acl_n, b_n);
-        for (int j = 0; j < NX; ++j) v += acl[j] * wbcast(w, pv, j);
-        pv = v;
-        wb.st(pv, 0u, row ? (unsigned)((CSF::SPV + li) * WL + kk) : junk);
-      }
-    }
-    wsync(w);
-    if (own() && k < N) {  // the feed-forward, stage-parallel
+    const MR_GLOBAL T* cb = rc + (int64_t)RC_STRIDE * WL;
+    const WBuf<T> wb(rc + (int64_t)RC_STRIDE * WL, (unsigned)CSF::NF * WL);
+    const bool row = ln < NX;
+    const int li = row ? ln : 0;
+    const unsigned junk = (unsigned)(CSF::SJUNK * WL + ln);
+    // one stage's operands: P_{k+1} row li, c_k, A_k column li (J column li, vehicle rows), B's J
+    // columns, K_k column li, Q_uu's factor, g_x[li], g_u
+    struct Ops {
+      T prow[NX], c[NX], acol[6], jb[12], kcol[NU], lq[6], gx, gu[NU];
+    };
+    auto ld = [&](int k, Ops& o) {
       const MR_GLOBAL T* Rk = R(k);
-      const MR_GLOBAL T* cb = rc + (int64_t)RC_STRIDE * WL;
-      T J[48], pc[NX], r[NU];
-      for (int i = 0; i < 48; ++i) J[i] = Rk[RCF::J + i];
-      for (int i = 0; i < NX; ++i) pc[i] = cb[(CSF::SPV + i) * WL + k + 1] + Cf(CSF::SPC + i);
-      apply_Bt(J, k, pc, r);
-      for (int a = 0; a < NU; ++a) r[a] += Cf(CSF::SG + NX + a);
-      // k = -Q_uu^-1 r with Q_uu = L L^T (L10, L20, L21, reciprocal pivots from the Riccati sweep)
-      const T L1 = Rk[RCF::LQ + 0], L3 = Rk[RCF::LQ + 1], L4 = Rk[RCF::LQ + 2];
-      const T iv[3] = {Rk[RCF::LQ + 3], Rk[RCF::LQ + 4], Rk[RCF::LQ + 5]};
-      const T Lf[6] = {T(0), L1, T(0), L3, L4, T(0)};
+      const MR_GLOBAL T* Rn = R(k + 1);
+      for (int l = 0; l < NX; ++l) o.prow[l] = Rn[RCF::P + pidx(li, l)];
+      for (int l = 0; l < NX; ++l) o.c[l] = cb[(CSF::SC + l) * WL + k];
+      for (int j = 0; j < 6; ++j) o.acol[j] = Rk[RCF::J + j * 8 + (li < 6 ? li : 0)];
+      for (int j = 0; j < 6; ++j) { o.jb[2 * j] = Rk[RCF::J + j * 8 + 6]; o.jb[2 * j + 1] = Rk[RCF::J + j * 8 + 7]; }
+      for (int a = 0; a < NU; ++a) o.kcol[a] = Rk[RCF::K + a * NX + li];
+      for (int q = 0; q < 6; ++q) o.lq[q] = Rk[RCF::LQ + q];
+      o.gx = cb[(CSF::SG + li) * WL + k];
+      for (int a = 0; a < NU; ++a) o.gu[a] = cb[(CSF::SG + NX + a) * WL + k];
+    };
+    T pv = cb[(CSF::SG + li) * WL + N];
+    wb.st(pv, 0u, row ? (unsigned)((CSF::SPV + li) * WL + N) : junk);
+    Ops nx;
+    if (N > 0) ld(N - 1, nx);
+    for (int k = N - 1; k >= 0; --k) {
+      const Ops o = nx;
+      if (k > 0) ld(k - 1, nx);
+      T pcl = pv;
+      for (int l = 0; l < NX; ++l) pcl += o.prow[l] * o.c[l];
+      T pc[NX];
+      wgather<T, NX>(w, pcl, pc);
+      // r = B^T pc + g_u (mr_solver.h apply_Bt), every lane
+      T r[NU] = {pc[7] + o.gu[0], pc[8] + o.gu[1], pc[6] + o.gu[2]};
+      if (k == 0) { r[0] += pc[9]; r[1] += pc[10]; }
+      for (int j = 0; j < 6; ++j) { r[0] += o.jb[2 * j] * pc[j]; r[1] += o.jb[2 * j + 1] * pc[j]; }
+      // (A^T pc)[li] (mr_solver.h apply_At)
+      T at;
+      if (li < 6) {
+        at = T(0);
+        for (int j = 0; j < 6; ++j) at += o.acol[j] * pc[j];
+      } else {
+        at = li == 6 ? pc[6] : ((li >= 9 && k > 0) ? (li == 9 ? pc[9] : pc[10]) : T(0));
+      }
+      pv = o.gx + at + o.kcol[0] * r[0] + o.kcol[1] * r[1] + o.kcol[2] * r[2];
+      wb.st(pv, 0u, row ? (unsigned)((CSF::SPV + li) * WL + k) : junk);
+      // k_k = -Q_uu^-1 r with Q_uu = L L^T (L10, L20, L21, reciprocal pivots from the Riccati sweep)
+      const T Lf[6] = {T(0), o.lq[0], T(0), o.lq[1], o.lq[2], T(0)};
+      const T iv[3] = {o.lq[3], o.lq[4], o.lq[5]};
       T kf[NU] = {-r[0], -r[1], -r[2]};
       lsolve3r(Lf, iv, kf);
       ltsolve3r(Lf, iv, kf);
-      for (int a = 0; a < NU; ++a) Cf(CSF::SK0 + a) = kf[a];
+      const T kv = ln == 0 ? kf[0] : (ln == 1 ? kf[1] : kf[2]);
+      wb.st(kv, 0u, ln < NU ? (unsigned)((CSF::SK0 + ln) * WL + k) : junk);
     }
     wsync(w);
   }
   // the SOC direction (mr_solver.h Solver::forward with soc set): SDZ, SDS, SDLAM, SDY, SDNU.
-  // dx_{k+1} = Acl_k dx_k + e_k with e_k = B_k k_k + c_k: e stage-parallel, the chain on lanes 0..10
-  // (dx_k to SDZ[0..10] of stage k), then du_k = k_k + K_k dx_k and the costate step
-  // dnu_k = pv_k + P_k dx_k stage-parallel
+  // The recursion du_k = k_k + K_k dx_k, dx_{k+1} = A_k dx_k + B_k du_k + c_k on lanes 0..10 (lane i:
+  // component i of dx, the others' by v_readlane; every lane forms du from K_k and k_k as uniform
+  // loads), dx_k to SDZ[0..10] and du_k to SDZ[11..13] of stage k; then stage-parallel the costate step
+  // dnu_k = pv_k + P_k dx_k, the rows' steps and the step limits.
   MR_SWEEP void forward_soc(T& ap, T& ad) {
     MR_UNIFORM_P();
     MR_ASSUME_LDS_STATE();
     const T tau = mr_max(T(0.99), T(1) - mu);
     const int N = wu(w, this->N);
     const MR_GLOBAL T* cb = rc + (int64_t)RC_STRIDE * WL;
-    if (own() && ln < N) {
-      const int k = ln;
-      const MR_GLOBAL T* Rk = R(k);
-      T J[48], kf[NU], tb[NX];
-      for (int i = 0; i < 48; ++i) J[i] = Rk[RCF::J + i];
-      for (int a = 0; a < NU; ++a) kf[a] = Cf(CSF::SK0 + a);
-      apply_B(J, k, kf, tb);
-      for (int i = 0; i < NX; ++i) Cf(CSF::SE + i) = tb[i] + Cf(CSF::SC + i);
-    }
-    wsync(w);
     {
       const WBuf<T> wb(rc + (int64_t)RC_STRIDE * WL, (unsigned)CSF::NF * WL);
       const bool row = ln < NX;
       const int li = row ? ln : 0;
       const unsigned junk = (unsigned)(CSF::SJUNK * WL + ln);
+      struct Ops {
+        T K[NU * NX], kf[NU], arow[6], brow[2], c;
+      };
+      auto ld = [&](int k, Ops& o) {
+        const MR_GLOBAL T* Rk = R(k);
+        for (int q = 0; q < NU * NX; ++q) o.K[q] = Rk[RCF::K + q];
+        for (int a = 0; a < NU; ++a) o.kf[a] = cb[(CSF::SK0 + a) * WL + k];
+        const int r6 = li < 6 ? li : 0;
+        for (int j = 0; j < 6; ++j) o.arow[j] = Rk[RCF::J + r6 * 8 + j];
+        o.brow[0] = Rk[RCF::J + r6 * 8 + 6];
+        o.brow[1] = Rk[RCF::J + r6 * 8 + 7];
+        o.c = cb[(CSF::SC + li) * WL + k];
+      };
       T dx = T(0);
       wb.st(dx, 0u, row ? (unsigned)((CSF::SDZ + li) * WL + 0) : junk);
-      T acl_n[NX], e_n;  // operands of the next stage loaded one stage ahead
-      auto ld = [&](int kk, T* acl, T& ee) {
-        for (int j = 0; j < NX; ++j) acl[j] = cb[(CSF::SACL + li * NX + j) * WL + kk];
-        ee = cb[(CSF::SE + li) * WL + kk];
-      };
-      if (N > 0) ld(0, acl_n, e_n);
-      for (int kk = 0; kk < N; ++kk) {
-        T acl[NX];
-        for (int j = 0; j < NX; ++j) acl[j] = acl_n[j];
-        T v = e_n;
-        if (kk + 1 < N) ld(kk + 1, acl_n, e_n);
-        for (int j = 0; j < NX; ++j) v += acl[j] * wbcast(w, dx, j);
-        dx = v;
-        wb.st(dx, 0u, row ? (unsigned)((CSF::SDZ + li) * WL + kk + 1) : junk);
+      Ops nx;
+      if (N > 0) ld(0, nx);
+      for (int k = 0; k < N; ++k) {
+        const Ops o = nx;
+        if (k + 1 < N) ld(k + 1, nx);
+        T dxa[NX];
+        wgather<T, NX>(w, dx, dxa);
+        T du[NU];
+        for (int a = 0; a < NU; ++a) {
+          T v = o.kf[a];
+          for (int j = 0; j < NX; ++j) v += o.K[a * NX + j] * dxa[j];
+          du[a] = v;
+        }
+        const T duv = ln == 0 ? du[0] : (ln == 1 ? du[1] : du[2]);
+        wb.st(duv, 0u, ln < NU ? (unsigned)((CSF::SDZ + NX + ln) * WL + k) : junk);
+        // row li of A dx + B du (mr_solver.h apply_A / apply_B)
+        T v;
+        if (li < 6) {
+          v = o.brow[0] * du[0] + o.brow[1] * du[1];
+          for (int j = 0; j < 6; ++j) v += o.arow[j] * dxa[j];
+        } else if (li == 6) {
+          v = dxa[6] + du[2];
+        } else if (li == 7) {
+          v = du[0];
+        } else if (li == 8) {
+          v = du[1];
+        } else {
+          v = k == 0 ? (li == 9 ? du[0] : du[1]) : (li == 9 ? dxa[9] : dxa[10]);
+        }
+        dx = v + o.c;
+        wb.st(dx, 0u, row ? (unsigned)((CSF::SDZ + li) * WL + k + 1) : junk);
       }
     }
     wsync(w);
@@ -2032,11 +2035,7 @@ struct WaveSolver {
       for (int i = 0; i < NZS; ++i) dz[i] = T(0);
       for (int i = 0; i < NX; ++i) dz[i] = Cf(CSF::SDZ + i);
       if (k < N)
-        for (int a = 0; a < NU; ++a) {
-          T v = Cf(CSF::SK0 + a);
-          for (int j = 0; j < NX; ++j) v += Rk[RCF::K + a * NX + j] * dz[j];
-          dz[NX + a] = v;
-        }
+        for (int a = 0; a < NU; ++a) dz[NX + a] = Cf(CSF::SDZ + NX + a);
       if (k > 0 || !MR_KKT_RESTATED)  // the costate (multiplier) step of x_k's rows (k = 0: the initial-state rows')
         for (int i = 0; i < NX; ++i) {
           T v = Cf(CSF::SPV + i);
@@ -2325,7 +2324,7 @@ struct WaveSolver {
     SolveOut out{2, 0, 0.0, 0.0, 0.0};
     double acc_kkt = 0.0, acc_obj = 0.0, acc_viol = 0.0;  // the stored acceptable point's measures
     T mu_prev = mu;
-    int acc_count = 0;
+    int acc_count = 0, stall = 0;
     // IPOPT's filter reset heuristic (filter_reset_trigger = 5, max_filter_resets = 5): after this many
     // successive iterations whose line search had a trial point rejected by the filter, clear it
     int filt_rej_iters = 0, filt_resets = 0;
@@ -2374,6 +2373,24 @@ struct WaveSolver {
         if (P.acc_iter > 0) {
           acc_count = acceptable(kkt) ? acc_count + 1 : 0;
           if (acc_count >= P.acc_iter) { out.status = 1; break; }
+        }
+        // fp32 only: at the mu floor, feasible to IPOPT's constr_viol_tol, without meeting
+        // the convergence tests for MR_F32_STALL iterations -> the fp64 solve's outcome there (the line
+        // search fails at the floor: the stored acceptable point or status 3).  In fp32 the constraint
+        // violation and phi carry rounding noise well above that line search's resolution, so trial
+        // points keep being accepted and the solve would run to max_iter instead.
+        if (sizeof(T) == 4 && MR_F32_STALL > 0) {
+          stall = (mu <= mu_min && mr_max(cw()->pr_eq, cw()->viol) <= T(IP_CONSTR_VIOL_TOL)) ? stall + 1 : 0;
+          if (stall >= MR_F32_STALL) {
+            if (cw()->have_acc) {
+              acc_restore();
+              out.status = 1;
+              out.kkt = acc_kkt; out.obj = acc_obj; out.viol = acc_viol;
+            } else {
+              out.status = 3;
+            }
+            break;
+          }
         }
       }
       if (it >= P.max_iter) { out.status = 2; break; }
@@ -2575,7 +2592,8 @@ struct WaveSolver {
         // current point acceptable -> "acceptable point reached"; almost feasible (theta <= 1e-2 tol) ->
         // the stored acceptable point or restoration failed; otherwise the restoration phase
         if (acceptable(kkt)) { out.status = 1; break; }
-        if (theta <= T(1e-2) * P.tol) {
+        if (theta <= T(1e-2) * P.tol ||
+            (sizeof(T) == 4 && mr_max(cw()->pr_eq, cw()->viol) <= T(IP_CONSTR_VIOL_TOL))) {  // fp32: feasible at its resolution
           if (cw()->have_acc) {
             acc_restore();
             out.status = 1;
