@@ -103,7 +103,95 @@ def cpu_baseline(name, batch, gpu_iters, budget_s):
             "iters_mean_cpu_fp64": float(it.mean()), "iters_mean_gpu_same_instances": float(gpu_iters[:n].mean()),
             "latency_1core_ms": {"p50": float(np.median(lat)), "p90": float(np.quantile(lat, 0.9)),
                                  "sample": "C1 + 100 C2 instances, one at a time, 1 thread"},
+            "fp32_ref_options": cpu_fp32_leg(name, batch, budget_s / 2),
+            "agent_call_1thread_ms": agent_call_cpu(),
             "other_configs": cpu_other_configs(budget_s)}
+
+
+AGENT_N, AGENT_TS = 15, 0.05  # /root/reference/agent.py:154 (N = 15), :181 (Ts = 0.05); dynamic model
+
+
+def _agent_instances(n=100):
+    """The agent's call (agent.py:171-183 -> control/MPC.py): B = 1, N = 15, the reference's dynamic model,
+    fp64, the reference's IPOPT options; inputs = the first n C2 instances (state, progress, centerline
+    polynomials and lane width drawn on the reference's track; no warm start)."""
+    from mpcracing import workload as wl
+    b = wl.make_batch("C2", limit=n)
+    return [{k: (v[..., i:i + 1].copy() if v is not None else None) for k, v in b.items()} for i in range(n)]
+
+
+def agent_call_gpu(local, n=100):
+    """GPU side of the agent's call on the same instances: per call p50/p90 of (a) the kernel alone with
+    the inputs resident (HIP-synchronised launch) and (b) the whole call from host arrays to host results
+    (H2D copies, launch, D2H of States / U / S_hat, what control.MPC does)."""
+    import torch
+    from mpcracing.batch import BatchSolver
+    s = BatchSolver(AGENT_N, "dyn", "fp64", False, AGENT_TS, max_batch=1, device=local, tol=1e-4, acceptable_tol=1e-2,
+                    acceptable_iter=15)
+    dev = torch.device("cuda", local)
+    kern, call, st = [], [], []
+    for sub in _agent_instances(n):
+        d = s.to_device(sub)
+        o = s.alloc_outputs(1)
+        s.launch(d, o)  # warm (first touch of this instance's buffers)
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        s.launch(d, o)
+        torch.cuda.synchronize(dev)
+        kern.append(time.perf_counter() - t)
+        t = time.perf_counter()
+        r = s.solve(sub)
+        _ = (r["X"].cpu(), r["U"].cpu(), r["S"].cpu(), r["status"].cpu())
+        call.append(time.perf_counter() - t)
+        st.append(int(o["status"][0]))
+    kern, call = np.array(kern) * 1e3, np.array(call) * 1e3
+    return {"kernel_ms": {"p50": float(np.median(kern)), "p90": float(np.quantile(kern, 0.9))},
+            "call_ms": {"p50": float(np.median(call)), "p90": float(np.quantile(call, 0.9))},
+            "status_hist": np.bincount(st, minlength=5).tolist()}
+
+
+def agent_call_cpu(n=100):
+    """CPU side: the scalar C++ solver (mr_solver.h Solver, the same IPM, fp64, same options), one thread,
+    one instance at a time, on the same instances."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import host_twin as ht
+    c = ht.config(AGENT_N, "dyn", "fp64", False, AGENT_TS, tol=1e-4, acceptable_iter=15, acceptable_tol=1e-2)
+    lat, st = [], []
+    for sub in _agent_instances(n):
+        t = time.perf_counter()
+        o = ht.solve(c, sub, nthreads=1, scalar=True)
+        lat.append(time.perf_counter() - t)
+        st.append(int(o["status"][0]))
+    lat = np.array(lat) * 1e3
+    return {"p50": float(np.median(lat)), "p90": float(np.quantile(lat, 0.9)),
+            "status_hist": np.bincount(st, minlength=5).tolist(), "threads": 1}
+
+
+def cpu_fp32_leg(name, batch, budget_s):
+    """The scalar solver in fp32 at the reference's options (tol 1e-4, acceptable 1e-2 / 15: the GPU line's
+    own precision and termination) on a bounded sample of the bench shard, all host threads."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import host_twin as ht
+    from mpcracing import workload as wl
+    cfg = wl.CONFIGS[name]
+    cores = _cpu_threads()
+    tyres = wl.tyre_coeffs(cfg["tyres"]) if cfg["tyres"] else None
+    c = ht.config(cfg["N"], cfg["model"], "fp32", cfg["lane"], cfg["Ts"], tol=1e-4, acceptable_iter=15,
+                  acceptable_tol=1e-2)
+    B = batch["s0"].shape[0]
+    chunk = 128 * cores
+    n, st = 0, []
+    t0 = time.perf_counter()
+    while n < B and time.perf_counter() - t0 < budget_s:
+        m = min(chunk, B - n)
+        sub = {k: (v[..., n:n + m].copy() if v is not None else None) for k, v in batch.items()}
+        o = ht.solve(c, sub, tyres=tyres, nthreads=cores, scalar=True)
+        st.append(o["status"])
+        n += m
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "solves/s", "cores": cores, "instances": n, "seconds": dt,
+            "status_hist": np.bincount(np.concatenate(st), minlength=5).tolist(),
+            "sample": f"first {n} instances of the {name} shard, scalar C++ fp32 build, tol 1e-4 / acceptable 1e-2 x 15"}
 
 
 def copy_bandwidth(dev, gib=1.0, reps=10):
@@ -361,6 +449,10 @@ def main():
             lat.append(time.perf_counter() - t)
         lat_b1_ms = float(np.median(lat[1:]) * 1e3)
 
+    agent = None
+    if not args.no_latency and not dry and rank == 0:
+        agent = agent_call_gpu(local)
+
     pipe = None
     if args.pipeline >= 2 and world == 1 and not dry and not args.no_latency:
         pipe = pipelined(args, solver, dev_in, out, batch, B, dev, local, args.pipeline)
@@ -377,13 +469,14 @@ def main():
         solves = tot[0]
         kavg = float(np.mean(kms)) / 1e3
         achieved = alg_bytes / kavg / 1e9  # this rank's algorithmic bytes per launch / avg launch time
-        traffic, traffic_src = None, None
+        traffic, traffic_src, compute = None, None, None
         pmc_path = os.path.join(REPO, "profiles", f"pmc_{args.config}.json")
         if os.path.exists(pmc_path):
             with open(pmc_path) as f:
                 pm = json.load(f)
             if pm.get("B") == B and pm.get("lib_sha") == _lib_sha():
                 traffic = pm.get("hbm_bytes_per_launch")
+                compute = pm.get("compute")
                 traffic_src = (f"{os.path.relpath(pmc_path, REPO)}: rocprofv3 --pmc passes of this command on "
                                f"the same libmpcracing.so build (sha {pm['lib_sha']})")
         line = {
@@ -416,10 +509,15 @@ def main():
                          "copy_gbs": copy_gbs,
                          "frac_vs_copy": (achieved / copy_gbs) if copy_gbs else None,
                          "copy_source": "measured in this run: 1 GiB fp32 device-to-device copy (torch copy_, "
-                                        "read + write bytes), HIP events"},
+                                        "read + write bytes), HIP events",
+                         "compute": compute},
         }
         if pipe is not None:
             line["pipelined"] = pipe
+        if agent is not None:
+            line["agent_call"] = dict(agent, config=f"agent.py:154,171-183: B = 1, N = {AGENT_N}, dyn, fp64, "
+                                                    f"Ts {AGENT_TS}, tol 1e-4 / acceptable 1e-2 x 15; the first 100 "
+                                                    "C2 instances (cpu side: cpu_baseline.agent_call_1thread_ms)")
         if dry:
             line["dry_run"] = True
         if world == 1 and not args.no_cpu_baseline and not dry:

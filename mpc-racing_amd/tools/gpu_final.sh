@@ -23,7 +23,8 @@ step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-latency
 step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-latency
 step pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-latency
-step pmc_sum 120 python mpc-racing_amd/tools/pmc_summary.py gpurun_out/prof/run_kernel_stats.csv gpurun_out/pmc_fetch/run_counter_collection.csv gpurun_out/pmc_write/run_counter_collection.csv gpurun_out/pmc_C4.json mr_wave_kernel $B C4
+step pmc_sq 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE -d gpurun_out/pmc_sq -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-latency
+step pmc_sum 120 python mpc-racing_amd/tools/pmc_summary.py gpurun_out/prof/run_kernel_stats.csv gpurun_out/pmc_fetch/run_counter_collection.csv gpurun_out/pmc_write/run_counter_collection.csv gpurun_out/pmc_C4.json mr_wave_kernel $B C4 gpurun_out/pmc_sq/run_counter_collection.csv
 # the bench line's roofline.traffic comes from profiles/pmc_C4.json when its library hash is this build's
 [ -s gpurun_out/pmc_C4.json ] && cp gpurun_out/pmc_C4.json profiles/pmc_C4.json
 step bench 600 python bench.py
@@ -34,4 +35,13 @@ fi
 step timeline 300 python -u mpc-racing_amd/tools/timeline_probe.py C4 1
 for c in C2 C3 C5; do
   step bench_$c 600 python bench.py --config $c --no-cpu-baseline
+done
+# kernel statistics and HBM traffic of C2 and C3 (same passes as C4's)
+for c in C2 C3; do
+  BC=$(python -c "import sys; sys.path.insert(0,'mpc-racing_amd'); from mpcracing import workload as wl; print(wl.CONFIGS['$c']['per_gpu'])")
+  step prof_$c 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$c -o run --output-format csv -- python bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-latency
+  step pmc_fetch_$c 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_$c -o run --output-format csv -- python bench.py --config $c --steps 1 --warmup 0 --no-cpu-baseline --no-latency
+  step pmc_write_$c 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_$c -o run --output-format csv -- python bench.py --config $c --steps 1 --warmup 0 --no-cpu-baseline --no-latency
+  step pmc_sum_$c 120 python mpc-racing_amd/tools/pmc_summary.py gpurun_out/prof_$c/run_kernel_stats.csv gpurun_out/pmc_fetch_$c/run_counter_collection.csv gpurun_out/pmc_write_$c/run_counter_collection.csv gpurun_out/pmc_$c.json mr_wave_kernel $BC $c
+  [ -s gpurun_out/pmc_$c.json ] && cp gpurun_out/pmc_$c.json profiles/pmc_$c.json
 done

@@ -68,9 +68,12 @@ def test_horizon_extremes_match_host_build(N):
     import host_twin as ht
     from mpcracing.batch import BatchSolver
     b = wl.make_batch("C2", limit=3)  # ragged: 3 instances
-    s = BatchSolver(N, "kin", "fp64", max_batch=5, tol=1e-10, acceptable_iter=0)
+    # the same options on both builds (acceptable_iter 15): at N = 63 the unscaled tests are out of reach,
+    # and with acceptable_iter 0 whether a line search fails at the mu floor (acceptable exit) or the
+    # solve runs to max_iter is decided by rounding, which the two builds do differently (FMA)
+    s = BatchSolver(N, "kin", "fp64", max_batch=5, tol=1e-10, acceptable_iter=15)
     o = {k: v.cpu().numpy() for k, v in s.solve(b).items()}
-    h = ht.solve(ht.config(N, "kin", "fp64", tol=1e-10), b, nthreads=4)
+    h = ht.solve(ht.config(N, "kin", "fp64", tol=1e-10, acceptable_iter=15), b, nthreads=4)
     assert (o["status"] == h["status"]).all(), (o["status"], h["status"])
     # at N = 63 the objective scaling is small enough that IPOPT's unscaled complementarity test fails at
     # the mu floor: the solves end "acceptable" (status 1) at the same point on both builds
