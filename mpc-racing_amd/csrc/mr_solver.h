@@ -99,6 +99,38 @@ MR_HD int hidx(int i, int j) {  // packed upper index of symmetric NZ x NZ
   if (i > j) { int t = i; i = j; j = t; }
   return i * NZ - (i * (i - 1)) / 2 + (j - i);
 }
+// Structural nonzeros of the stage Hessian (entries any stage, model, lane setting or phase can make
+// nonzero): the vehicle dynamics block {X, Y, psi, vx, vy, r, thr, steer} (Dyn::fjh), the contouring / lag
+// cost and lane rows on {X, Y, S} (stage_cost, lane rows), the rows' pairs (thr, p_thr), (steer, p_steer)
+// (also the steering-rate cost), (w_thr, thr), (w_steer, steer), and the diagonal (row barriers,
+// restoration proximity term).  48 of the 105 packed entries; the wave kernel's stage record stores only
+// these (mr_wave.h RCF::H, compact index hcidx).
+MR_HD constexpr bool h_dyn(int a) { return a <= 5 || a == 11 || a == 12; }
+MR_HD constexpr bool h_xys(int a) { return a == 0 || a == 1 || a == 6; }
+MR_HD constexpr bool h_struct(int i, int j) {
+  return i == j || (h_dyn(i) && h_dyn(j)) || (h_xys(i) && h_xys(j)) || (i == 7 && j == 11) || (i == 11 && j == 7) ||
+         (i == 8 && j == 12) || (i == 12 && j == 8) || (i == 9 && j == 11) || (i == 11 && j == 9) ||
+         (i == 10 && j == 12) || (i == 12 && j == 10);
+}
+// compact index of the structural entry (i, j) (either order) in row-major upper order, -1 if not structural
+MR_HD constexpr int hcidx(int i, int j) {
+  if (i > j) { const int t = i; i = j; j = t; }
+  if (!h_struct(i, j)) return -1;
+  int n = 0;
+  for (int a = 0; a < NZ; ++a)
+    for (int b = a; b < NZ; ++b) {
+      if (a == i && b == j) return n;
+      if (h_struct(a, b)) ++n;
+    }
+  return -1;
+}
+constexpr int NHC = [] {
+  int n = 0;
+  for (int a = 0; a < NZ; ++a)
+    for (int b = a; b < NZ; ++b) n += h_struct(a, b) ? 1 : 0;
+  return n;
+}();
+static_assert(NHC == 48, "structural nonzeros of the stage Hessian");
 MR_HD int pidx(int i, int j) {  // packed upper index of symmetric NX x NX
   if (i > j) { int t = i; i = j; j = t; }
   return i * NX - (i * (i - 1)) / 2 + (j - i);

@@ -100,7 +100,7 @@ constexpr int NHD = 17;
 // (Jacobian, defect, Hessian, gradients), then the Riccati sweep's outputs.
 struct RCF {
   enum {
-    J = 0, C = J + 48, H = C + NX, G0 = H + NH, G1 = G0 + NZ,
+    J = 0, C = J + 48, H = C + NX, G0 = H + NHC, G1 = G0 + NZ,  // H: the 48 structural entries (hcidx)
     HD = G1 + NZ, GD = HD + NHD,  // the slack shift's pattern (hd_slot) and sum a (d - s) (delta_s)
     P = GD + NZ, PV0 = P + NP, K = PV0 + NX, K0 = K + NU * NX,
     LQ = K0 + NU,  // Q_uu's Cholesky factor: L10, L20, L21 and the reciprocal pivots (SOC re-solves)
@@ -111,9 +111,12 @@ struct RCF {
 #ifdef MR_RC_STRIDE_FORCE
 constexpr int RC_STRIDE = MR_RC_STRIDE_FORCE;  // A/B option (record footprint)
 #else
-constexpr int RC_STRIDE = (RCF::NF + 15) / 16 * 16;  // words; 16-word (64 B) multiple (320)
+constexpr int RC_STRIDE = (RCF::NF + 15) / 16 * 16;  // words; 16-word (64 B) multiple (304)
 #endif
 static_assert(RCF::NF <= RC_STRIDE, "record");
+#ifndef MR_RC_STRIDE_FORCE
+static_assert(RC_STRIDE == 304, "record stride (DESIGN.md §3)");
+#endif
 // Cold per-stage fields [f][64] after the records: touched only by the watchdog (its snapshot of the
 // iterate and the search direction) and the restoration phase (the relaxations p, n of the rows and
 // of the 6 vehicle dynamics rows, their bound duals and steps, the rows' equality multipliers y, the
@@ -503,7 +506,11 @@ struct WaveSolver {
         for (int a = 0; a < 3; ++a)
           for (int bb = a; bb < 3; ++bb) H[hidx(id3[a], id3[bb])] += e.gC[a] * e.gC[bb];
       }
-      for (int i = 0; i < NH; ++i) Rk[RCF::H + i] = H[i];
+#pragma unroll
+      for (int a = 0; a < NZ; ++a)
+#pragma unroll
+        for (int bb = a; bb < NZ; ++bb)
+          if (h_struct(a, bb)) Rk[RCF::H + hcidx(a, bb)] = H[hidx(a, bb)];
       for (int i = 0; i < NZ; ++i) { Rk[RCF::G0 + i] = g[i]; Rk[RCF::G1 + i] = T(0); Rk[RCF::GD + i] = T(0); }
       for (int q = 0; q < NHD; ++q) Rk[RCF::HD + q] = T(0);
       for (int i = 0; i < NX; ++i) Rk[RCF::C + i] = T(0);
@@ -879,7 +886,21 @@ struct WaveSolver {
           if (i < NX ? k >= 1 : k < N) st_l = mr_max(st_l, mr_abs(sti));
         }
       }
-      for (int i = 0; i < NH; ++i) rbe.st(H[i], 0u, Rk + RCF::H + i);
+#if !MR_DEVICE_BUILD
+      for (int a = 0; a < NZ; ++a)  // host build: the structural pattern holds (tests run every model / phase)
+        for (int bb = a; bb < NZ; ++bb)
+          if (!h_struct(a, bb) && H[hidx(a, bb)] != T(0)) {
+            fprintf(stderr, "mr_wave.h: stage Hessian entry (%d, %d) outside h_struct\n", a, bb);
+            abort();
+          }
+#endif
+      // the structural entries only, contiguous (48 words instead of 105: the record is written back by
+      // whole lines, so skipped zeros inside the packed triangle saved nothing -- a compact layout does)
+#pragma unroll
+      for (int a = 0; a < NZ; ++a)
+#pragma unroll
+        for (int bb = a; bb < NZ; ++bb)
+          if (h_struct(a, bb)) rbe.st(H[hidx(a, bb)], 0u, Rk + RCF::H + hcidx(a, bb));
       for (int i = 0; i < NZ; ++i) {
         rbe.st(T((double)g0[i] + dd[i]), 0u, Rk + RCF::G0 + i);
         rbe.st(g1[i], 0u, Rk + RCF::G1 + i);
@@ -1015,7 +1036,9 @@ struct WaveSolver {
     for (int v = 0; v < 4; ++v) {
       const int a = drow(g, v);
       const int a_ = a < NZ ? a : 0;
-      fp.off[4 + v] = a < NZ ? (c < NZ ? RCF::H + hidx(a_, c) : (c == 14 ? RCF::G0 + a_ : RCF::G1 + a_)) : RCF::CZERO;
+      fp.off[4 + v] = a < NZ ? (c < NZ ? (h_struct(a_, c) ? RCF::H + hcidx(a_, c) : RCF::CZERO)
+                                        : (c == 14 ? RCF::G0 + a_ : RCF::G1 + a_))
+                             : RCF::CZERO;
       if (a < NZ && a == c && delta_var(a)) fp.dlt |= 1u << v;
       {
         const int lo_ = a < c ? a : c, hi_ = a < c ? c : a;
@@ -1031,18 +1054,21 @@ struct WaveSolver {
       fp.lp[v] = sq ? a * LDS_LD + c : (c14 ? a * LDS_LD + 11 : junk_l);
     }
   }
+  // DS: the slack shift's gathers (8..11) only when delta > 0 (a delta = 0 factorisation skips them)
+  template <bool DS>
   static MR_HD void frag_load(const WBuf<T>& rb, unsigned ro, const FragPlan& fp, T* raw) {
 #pragma unroll
-    for (int q = 0; q < NGATHER; ++q) raw[q] = rb.ld(ro, (unsigned)fp.off[q]);
+    for (int q = 0; q < (DS ? NGATHER : 8); ++q) raw[q] = rb.ld(ro, (unsigned)fp.off[q]);
   }
   // operands straight from the gathered words (constants come from the record's constant slots); the
   // inertia correction: delta on the reference's variables (dd) and delta_s = delta on the slacks (delta x
   // the gathered slack-shift entry)
+  template <bool DS>
   static MR_HD void frag_finish(const T* dd, T delta, const T* raw, T* eb, T* hc) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) eb[s] = raw[s];
 #pragma unroll
-    for (int v = 0; v < 4; ++v) hc[v] = raw[4 + v] + dd[v] + delta * raw[8 + v];
+    for (int v = 0; v < 4; ++v) hc[v] = raw[4 + v] + dd[v] + (DS ? delta * raw[8 + v] : T(0));
   }
 
   // ---------------- sweep 2: Riccati factorisation on the matrix cores ----------------
@@ -1101,7 +1127,9 @@ struct WaveSolver {
     return true;
   }
 
-  template <bool RESTO>
+  // DS: delta > 0 in the regular phase (the slack shift delta_s = delta enters); false for delta = 0 and in
+  // the restoration phase, whose records carry no slack-shift data
+  template <bool RESTO, bool DS = false>
   MR_SWEEP bool riccati(T delta, T mu) {
     MR_ASSUME_LDS_STATE();
     const int l = ln, N = wu(w, this->N), g = l >> 4, c = l & 15;
@@ -1126,11 +1154,11 @@ struct WaveSolver {
     // gather is an Infinity-Cache / HBM round trip (the 8 192 instances' records do not fit the L2),
     // longer than one stage's arithmetic
     T raw_a[NGATHER], raw_b[NGATHER], raw_c[NGATHER];
-    frag_load(rb, R(N - 1), fp, raw_a);
-    frag_load(rb, R(N >= 2 ? N - 2 : 0), fp, raw_b);
+    frag_load<DS>(rb, R(N - 1), fp, raw_a);
+    frag_load<DS>(rb, R(N >= 2 ? N - 2 : 0), fp, raw_b);
 #if MR_RIC_AHEAD == 3
     T raw_d[NGATHER];
-    frag_load(rb, R(N >= 3 ? N - 3 : 0), fp, raw_c);
+    frag_load<DS>(rb, R(N >= 3 ? N - 3 : 0), fp, raw_c);
 #endif
     {  // terminal cost-to-go: P_N = H_N,xx + delta I, p_N = g_N.  Branch-free (lanes >= NX write
        // discard slots), so at least as many memory ops follow the first prefetch on this path as
@@ -1141,11 +1169,11 @@ struct WaveSolver {
       T hv[NX], hdv[NX];  // all loads ahead of the stores (the compiler cannot disambiguate H from P)
 #pragma unroll
       for (int j = 0; j < NX; ++j) {
-        hv[j] = rb.ld(Rn, RCF::H + hidx(lr, j));
+        hv[j] = rb.ld(Rn, h_struct(lr, j) ? RCF::H + hcidx(lr, j) : RCF::CZERO);
         const int hs = hd_slot(lr < j ? lr : j, lr < j ? j : lr);
-        hdv[j] = rb.ld(Rn, hs >= 0 ? RCF::HD + hs : RCF::CZERO);
+        hdv[j] = DS ? rb.ld(Rn, hs >= 0 ? RCF::HD + hs : RCF::CZERO) : T(0);
       }
-      const T p0 = rb.ld(Rn, RCF::G0 + lr) + delta * rb.ld(Rn, RCF::GD + lr), p1 = rb.ld(Rn, RCF::G1 + lr);
+      const T p0 = rb.ld(Rn, RCF::G0 + lr) + (DS ? delta * rb.ld(Rn, RCF::GD + lr) : T(0)), p1 = rb.ld(Rn, RCF::G1 + lr);
 #pragma unroll
       for (int j = 0; j < NX; ++j) {
         const T v = hv[j] + delta * hdv[j] + (l == j && delta_var(j) ? delta : T(0));
@@ -1165,10 +1193,10 @@ struct WaveSolver {
       // stage offsets as visibly wave-uniform values (SGPR soffsets, not per-lane waterfall loops)
       const unsigned Rk = (unsigned)wu(w, (int)R(k));
       T eb[4], dq[4];
-      frag_finish(dd, delta, raw_use, eb, dq);
+      frag_finish<DS>(dd, delta, raw_use, eb, dq);
 #pragma unroll
       for (int v = 0; v < 4; ++v) dq[v] = (dq[v] + s14 * wrow_next(w, dq[v])) * k15;  // g0 + mu g1 | 0
-      frag_load(rb, (unsigned)wu(w, (int)R(k >= MR_RIC_AHEAD ? k - MR_RIC_AHEAD : 0)), fp, raw_fill);  // unconditional: k < AHEAD re-read stage 0's record
+      frag_load<DS>(rb, (unsigned)wu(w, (int)R(k >= MR_RIC_AHEAD ? k - MR_RIC_AHEAD : 0)), fp, raw_fill);  // unconditional: k < AHEAD re-read stage 0's record
       // X = P^ E^  (A fragment s: P^[c][4s+g])
       // two independent 2-MFMA accumulation chains (k = 0..7 | 8..15) instead of one 4-long
       // dependent chain: half the MFMA latency on the stage's critical path
@@ -2415,12 +2443,17 @@ struct WaveSolver {
         MR_CNT(6);
 #if MR_PHASE_CYCLES
         const unsigned long long tr0 = trace ? MR_CLOCK() : 0ull;
-        const bool rok = rs ? riccati<true>(delta, mu) : riccati<false>(delta, mu);
+        const bool rok = rs ? riccati<true>(delta, mu)
+                            : (delta > T(0) ? riccati<false, true>(delta, mu) : riccati<false, false>(delta, mu));
         if (trace && !rok) { tsub[4] += MR_CLOCK() - tr0; tsub[5] += 1; }
         if (rok) { fact_ok = true; break; }
 #else
         MR_STAT(st_fact++);
-        if (rs ? riccati<true>(delta, mu) : riccati<false>(delta, mu)) { fact_ok = true; break; }
+        if (rs ? riccati<true>(delta, mu)
+               : (delta > T(0) ? riccati<false, true>(delta, mu) : riccati<false, false>(delta, mu))) {
+          fact_ok = true;
+          break;
+        }
 #endif
         if (first) {
           delta = delta_last == T(0) ? T(1e-4) : mr_max(T(1e-20), delta_last / T(3));

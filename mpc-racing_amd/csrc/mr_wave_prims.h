@@ -15,6 +15,7 @@
 
 #if !MR_DEVICE_BUILD
 #include <ucontext.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <cmath>
