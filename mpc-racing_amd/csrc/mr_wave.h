@@ -512,7 +512,26 @@ struct WaveSolver {
         for (int bb = a; bb < NZ; ++bb)
           if (h_struct(a, bb)) Rk[RCF::H + hcidx(a, bb)] = H[hidx(a, bb)];
       for (int i = 0; i < NZ; ++i) { Rk[RCF::G0 + i] = g[i]; Rk[RCF::G1 + i] = T(0); Rk[RCF::GD + i] = T(0); }
-      for (int q = 0; q < NHD; ++q) Rk[RCF::HD + q] = T(0);
+      // the slack shift's pattern of the box / rate / wrap rows (eval_sweep hd): fixed by the stage's rows,
+      // written once here; the evaluation sweep rewrites it only where the lane row adds its gC gC^T
+      {
+        T hdc[NHD];
+#pragma unroll
+        for (int q = 0; q < NHD; ++q) hdc[q] = T(0);
+#pragma unroll
+        for (int r = 0; r < NROW; ++r) {
+          if (!act[2 * r]) continue;
+          const T hdw = r < 2 ? T(2) : T(1);
+#pragma unroll
+          for (int a = 0; a < RN(r); ++a)
+#pragma unroll
+            for (int bb = 0; bb < RN(r); ++bb) {
+              const int ia = RI(r, a), ib = RI(r, bb);
+              if (ia <= ib) hdc[hd_slot(ia, ib)] += hdw * T(RS(a)) * T(RS(bb));
+            }
+        }
+        for (int q = 0; q < NHD; ++q) Rk[RCF::HD + q] = hdc[q];
+      }
       for (int i = 0; i < NX; ++i) Rk[RCF::C + i] = T(0);
     }
     wsync(w);
@@ -904,9 +923,13 @@ struct WaveSolver {
       for (int i = 0; i < NZ; ++i) {
         rbe.st(T((double)g0[i] + dd[i]), 0u, Rk + RCF::G0 + i);
         rbe.st(g1[i], 0u, Rk + RCF::G1 + i);
-        rbe.st(gd[i], 0u, Rk + RCF::GD + i);
       }
-      for (int q = 0; q < NHD; ++q) rbe.st(hd[q], 0u, Rk + RCF::HD + q);
+      if constexpr (!RESTO) {  // the slack shift (delta_s) enters the regular phase's factorisations only
+        for (int i = 0; i < NZ; ++i) rbe.st(gd[i], 0u, Rk + RCF::GD + i);
+        // its pattern is the rows' constant one (ls_record) unless the lane row adds gC gC^T
+        if (lane_active(P, k))
+          for (int q = 0; q < NHD; ++q) rbe.st(hd[q], 0u, Rk + RCF::HD + q);
+      }
     }
     if constexpr (refk) {
       // S_k = S_k + Delta-S_{k-1} - Delta-S_k; U_k = u_k + p_{k+1} (U_0: + every w_j); lanes > N hold zeros
