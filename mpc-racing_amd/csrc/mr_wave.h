@@ -1660,8 +1660,9 @@ struct WaveSolver {
   // Solver::backtrack): alpha = a0, a0/2, ... while alpha > a_min (the first trial always); acceptance =
   // theta_max, then (f-type at the test step size with theta_ref <= theta_min) Armijo or sufficient
   // decrease (Compare_le, obj_max_inc), then the filter.  Modes (flags):
-  //   LS_WD     watchdog: one trial, judged at the watchdog's step size wd_atest;
-  //   LS_FORCE  one trial, stored whatever its acceptance (the watchdog's tentative full step);
+  //   LS_WD     one trial, judged at the given test step size (the watchdog's, or the SOC's original), and
+  //             stored whatever its acceptance (the watchdog's tentative full step needs no re-evaluation);
+  //   LS_FORCE  one trial, stored whatever its acceptance;
   //   LS_ACC    one trial, accumulate its constraint values into the SOC right-hand sides
   //             (SC = acc SC + c(trial), SR = acc SR + (d - s)(trial)), nothing stored;
   //   otherwise backtracking; a rejected first trial (a0 = the fraction-to-boundary step, theta not
@@ -1832,7 +1833,11 @@ struct WaveSolver {
           store = true;
           break;
         }
-        if (mode & LS_WD) break;
+        if (mode & LS_WD) {  // the single trial is stored either way: the watchdog takes it anyway if its
+          store = true;      // trial budget lasts (no re-evaluation); otherwise the point is overwritten
+          flags |= fin ? LSR_FIN : 0;
+          break;
+        }
         if (!RESTO && !(mode & LS_NOSOC) && fin && n == 0 && alpha == a_max && theta <= th_t) {
           flags |= LSR_NEED_SOC;  // the caller runs the second-order corrections, then resumes at alpha/2
           break;
@@ -2569,8 +2574,7 @@ struct WaveSolver {
           C->in_wd = 0;
           C->wd_short = 0;
         } else if (++C->wd_trial <= MR_WD_TRIAL_MAX) {
-          take_anyway = true;  // the full step is taken tentatively
-          line_search<false, false>(th, ph, gphi, th_pow, ap, ap, ap, 0, LS_FORCE, ap, T(-1));
+          take_anyway = true;  // the full step is taken tentatively (LS_WD stored that trial point already)
         } else {
           // back to the watchdog point: its iterate and direction, a regular backtracking line search
           // that skips the full step

@@ -218,3 +218,25 @@ def test_fp32_close_to_fp64():
     assert ok.sum() >= 4
     dU = np.abs(o32["U"] - o64["U"])[:, :-1, ok]
     assert np.median(dU) < 1e-3 and dU.max() < 5e-2
+
+
+def test_second_order_corrections_wave_matches_scalar():
+    """IPOPT's linear second-order corrections (up to 4 per line search, continued while theta falls by
+    kappa_soc) take the same decisions in the emulated wave kernel as in the scalar solver: C4 instance
+    4765 at the reference's options in fp64 (a long solve at mu 2.8e-3 whose line searches reject the
+    full step and correct it) -- every iteration's kkt, mu, alpha, delta, theta, phi and marker equal to
+    1e-6 over 150 iterations, with corrections accepted (marker >= 100)."""
+    cfg = wl.CONFIGS["C4"]
+    i = 4765
+    b = wl.make_batch("C4", limit=i + 1)
+    sub = {k: (v[..., i:i + 1].copy() if v is not None else None) for k, v in b.items()}
+    c = ht.config(cfg["N"], cfg["model"], "fp64", cfg["lane"], cfg["Ts"], tol=1e-4, acceptable_iter=15,
+                  acceptable_tol=1e-2, max_iter=150)
+    a = ht.solve(c, sub, nthreads=1, scalar=True, trace_instance=0, trace_cap=200)
+    w = ht.solve(c, sub, nthreads=1, scalar=False, trace_instance=0, trace_cap=200)
+    n = int(a["iters"][0])
+    assert int(w["iters"][0]) == n and int(w["status"][0]) == int(a["status"][0])
+    ta, tw = a["trace"][:n], w["trace"][:n]
+    assert (ta[:, 7] >= 100).sum() >= 5  # corrections accepted
+    np.testing.assert_array_equal(ta[:, 7], tw[:, 7])
+    np.testing.assert_allclose(tw[:, :7], ta[:, :7], rtol=1e-6, atol=1e-12)
