@@ -131,6 +131,30 @@ constexpr int NHC = [] {
   return n;
 }();
 static_assert(NHC == 48, "structural nonzeros of the stage Hessian");
+// packed index (hidx) of the q-th structural entry: the compact store / gather loops run over q with
+// compile-time table entries (no index search at run time)
+struct HCTab {
+  int p[NHC];
+};
+constexpr HCTab make_hctab() {
+  HCTab t{};
+  int n = 0;
+  for (int a = 0; a < NZ; ++a)
+    for (int b = a; b < NZ; ++b)
+      if (h_struct(a, b)) t.p[n++] = a * NZ - (a * (a - 1)) / 2 + (b - a);
+  return t;
+}
+constexpr HCTab HCT = make_hctab();
+// packed index -> compact index (-1: structural zero), for run-time lookups (the Riccati's gather plan)
+struct HCInv {
+  int c[NH];
+};
+constexpr HCInv make_hcinv() {
+  HCInv t{};
+  for (int i = 0; i < NH; ++i) t.c[i] = -1;
+  for (int q = 0; q < NHC; ++q) t.c[HCT.p[q]] = q;
+  return t;
+}
 MR_HD int pidx(int i, int j) {  // packed upper index of symmetric NX x NX
   if (i > j) { int t = i; i = j; j = t; }
   return i * NX - (i * (i - 1)) / 2 + (j - i);

@@ -507,10 +507,7 @@ struct WaveSolver {
           for (int bb = a; bb < 3; ++bb) H[hidx(id3[a], id3[bb])] += e.gC[a] * e.gC[bb];
       }
 #pragma unroll
-      for (int a = 0; a < NZ; ++a)
-#pragma unroll
-        for (int bb = a; bb < NZ; ++bb)
-          if (h_struct(a, bb)) Rk[RCF::H + hcidx(a, bb)] = H[hidx(a, bb)];
+      for (int q = 0; q < NHC; ++q) Rk[RCF::H + q] = H[HCT.p[q]];
       for (int i = 0; i < NZ; ++i) { Rk[RCF::G0 + i] = g[i]; Rk[RCF::G1 + i] = T(0); Rk[RCF::GD + i] = T(0); }
       // the slack shift's pattern of the box / rate / wrap rows (eval_sweep hd): fixed by the stage's rows,
       // written once here; the evaluation sweep rewrites it only where the lane row adds its gC gC^T
@@ -916,10 +913,7 @@ struct WaveSolver {
       // the structural entries only, contiguous (48 words instead of 105: the record is written back by
       // whole lines, so skipped zeros inside the packed triangle saved nothing -- a compact layout does)
 #pragma unroll
-      for (int a = 0; a < NZ; ++a)
-#pragma unroll
-        for (int bb = a; bb < NZ; ++bb)
-          if (h_struct(a, bb)) rbe.st(H[hidx(a, bb)], 0u, Rk + RCF::H + hcidx(a, bb));
+      for (int q = 0; q < NHC; ++q) rbe.st(H[HCT.p[q]], 0u, Rk + RCF::H + q);
       for (int i = 0; i < NZ; ++i) {
         rbe.st(T((double)g0[i] + dd[i]), 0u, Rk + RCF::G0 + i);
         rbe.st(g1[i], 0u, Rk + RCF::G1 + i);
@@ -1052,6 +1046,7 @@ struct WaveSolver {
   }
   static MR_HD void frag_plan(int lane, FragPlan& fp) {
     const int g = lane >> 4, c = lane & 15;
+    constexpr HCInv hci = make_hcinv();
     fp.dlt = 0u;
 #pragma unroll
     for (int s = 0; s < 4; ++s) fp.off[s] = ehat_slot(4 * s + g, c, true);
@@ -1059,7 +1054,8 @@ struct WaveSolver {
     for (int v = 0; v < 4; ++v) {
       const int a = drow(g, v);
       const int a_ = a < NZ ? a : 0;
-      fp.off[4 + v] = a < NZ ? (c < NZ ? (h_struct(a_, c) ? RCF::H + hcidx(a_, c) : RCF::CZERO)
+      const int hc = (a < NZ && c < NZ) ? hci.c[hidx(a_, c)] : -1;
+      fp.off[4 + v] = a < NZ ? (c < NZ ? (hc >= 0 ? RCF::H + hc : RCF::CZERO)
                                         : (c == 14 ? RCF::G0 + a_ : RCF::G1 + a_))
                              : RCF::CZERO;
       if (a < NZ && a == c && delta_var(a)) fp.dlt |= 1u << v;
@@ -1166,6 +1162,7 @@ struct WaveSolver {
     wsync_lds(w);
     FragPlan fp;
     frag_plan(l, fp);
+    constexpr HCInv hci = make_hcinv();
     T dd[4];
 #pragma unroll
     for (int v = 0; v < 4; ++v) dd[v] = ((fp.dlt >> v) & 1u) ? delta : T(0);
@@ -1192,7 +1189,7 @@ struct WaveSolver {
       T hv[NX], hdv[NX];  // all loads ahead of the stores (the compiler cannot disambiguate H from P)
 #pragma unroll
       for (int j = 0; j < NX; ++j) {
-        hv[j] = rb.ld(Rn, h_struct(lr, j) ? RCF::H + hcidx(lr, j) : RCF::CZERO);
+        hv[j] = rb.ld(Rn, hci.c[hidx(lr, j)] >= 0 ? RCF::H + hci.c[hidx(lr, j)] : RCF::CZERO);
         const int hs = hd_slot(lr < j ? lr : j, lr < j ? j : lr);
         hdv[j] = DS ? rb.ld(Rn, hs >= 0 ? RCF::HD + hs : RCF::CZERO) : T(0);
       }
