@@ -965,7 +965,7 @@ struct WaveSolver {
     me = refk ? 6 * N + 7 : NX * (N + 1);
     wsync(w);  // stage records visible to every lane before the Riccati sweep
 #if MR_PHASE_CYCLES
-    if (trace) { tsub[2] += te1 - te0; tsub[3] += MR_CLOCK() - te1; }
+    (void)te0; (void)te1;  // (tsub[2..3] carry forward_soc's chain / stage-parallel split)
 #endif
   }
 
@@ -1313,21 +1313,11 @@ struct WaveSolver {
   }
 
 
-  // ---------------- sweep 3: forward substitution, slack/dual steps ----------------
-  //   Sequential part: per stage, three lane groups share one 11-term dot with dx_k (gathered from
-  //   lanes 0..10): [A | c] rows -> A dx_k + c, P_k rows -> the costate step, K_k rows -> du_k =
-  //   K_k dx_k + k; then dx_{k+1} = A dx_k + c + B du_k (stage Jacobian from the record,
-  //   no closed-loop map).  Then stage-parallel: slack / multiplier steps and the step limits.
-  MR_SWEEP void forward(T& ap, T& ad, T& gphi) {
-    MR_UNIFORM_P();
-    MR_ASSUME_LDS_STATE();
-#if MR_PHASE_CYCLES
-    const unsigned long long tf0 = trace ? MR_CLOCK() : 0ull;
-#endif
-    const T mu = this->mu;
-    const T tau = mr_max(T(0.99), T(1) - mu);
-    T dz[NZS];
-    for (int i = 0; i < NZS; ++i) dz[i] = T(0);
+  // The forward recursion of sweep 3 (dz of the lane's stage, from LDS): the Newton direction, or with SOCM
+  // the second-order correction's (feed-forward k_soc, constant c_soc, costate p_soc from the SOC's cold
+  // fields, its costate step to SDNU) -- the same lane-group recursion for both.
+  template <bool SOCM>
+  MR_HD void fwd_recursion(T* dz) {
     {
       const int N = wu(this->w, this->N), ln = this->ln;  // N wave-uniform: the stage offsets are soffsets
       const Wv w = this->w;
@@ -1355,6 +1345,12 @@ struct WaveSolver {
 #pragma unroll
       for (int a = 0; a < NU; ++a) boff[a] = ehat_slot(r0, NX + a, g0r);
       c0off = g0r ? ehat_slot(r0, 14, true) : (g1r ? RCF::PV0 + r : (g2r ? RCF::K0 + r : RCF::CZERO));
+      // SOCM: the constants come from the SOC's cold fields (c_soc, its costate vector, its feed-forward)
+      // of stage kk, one extra gather per stage; lanes without a row keep the record's zero slot
+      const bool cold_c = SOCM && (g0r | g1r | g2r);
+      const unsigned cold0 = (unsigned)(SSF::NF * WL) + (unsigned)RC_STRIDE * WL;  // cold fields' base word
+      const unsigned ccoff = g0r ? (unsigned)(CSF::SC + r) * WL : (g1r ? (unsigned)(CSF::SPV + r) * WL
+                                                                       : (unsigned)(CSF::SK0 + (g2r ? r : 0)) * WL);
       static_assert(3 * WL <= LP_OFF + 16 * LDS_LD, "du staging");
       // LDS target of each lane's step result (branch-free, one store): group 0 dx_{k+1}[r] at
       // LDX[(k + 1) 12 + r] (row N + 1 <= 64; N = 63: the discard slots), group 2 du_k[r] at
@@ -1377,6 +1373,10 @@ struct WaveSolver {
 #pragma unroll
         for (int a = 0; a < NU; ++a) f.bw[a] = wb.ld(ro, (unsigned)boff[a]);
         f.c0 = wb.ld(ro, (unsigned)c0off);
+        if constexpr (SOCM) {
+          const T cc = wb.ld(cold0 + (unsigned)kk, ccoff);
+          f.c0 = cold_c ? cc : f.c0;
+        }
       };
       auto fstep = [&](int k, const FwdRow& f) {
         T dxv[NX];
@@ -1403,7 +1403,9 @@ struct WaveSolver {
         dxi = g0r ? accx : T(0);
         lds[lbase + lstep * k] = g0r ? accx : acc;
         const bool dn = g1r & (k >= 1 || !MR_KKT_RESTATED);  // k = 0: the initial-state rows' multiplier step
-        if constexpr (SSL) {
+        if constexpr (SOCM) {  // the SOC's costate step to its cold field (branch-free: others the discard slot)
+          wb.st(acc, (unsigned)k, dn ? cold0 + (unsigned)(CSF::SDNU + r) * WL : R(k) + RCF::JUNK - (unsigned)k);
+        } else if constexpr (SSL) {
           if (dn) ss[(SSF::DNU + r) * WL + k] = acc;
         } else {  // branch-free: other lanes write stage k's record discard slot
           wb.st(acc, (unsigned)k, dn ? (unsigned)(SSF::DNU + r) * WL : R(k) + RCF::JUNK - (unsigned)k);
@@ -1429,6 +1431,24 @@ struct WaveSolver {
       if (ln < N)
         for (int a = 0; a < NU; ++a) dz[NX + a] = lds[LX_OFF + 3 * ln + a];
     }
+  }
+
+  // ---------------- sweep 3: forward substitution, slack/dual steps ----------------
+  //   Sequential part: per stage, three lane groups share one 11-term dot with dx_k (gathered from
+  //   lanes 0..10): [A | c] rows -> A dx_k + c, P_k rows -> the costate step, K_k rows -> du_k =
+  //   K_k dx_k + k; then dx_{k+1} = A dx_k + c + B du_k (stage Jacobian from the record,
+  //   no closed-loop map).  Then stage-parallel: slack / multiplier steps and the step limits.
+  MR_SWEEP void forward(T& ap, T& ad, T& gphi) {
+    MR_UNIFORM_P();
+    MR_ASSUME_LDS_STATE();
+#if MR_PHASE_CYCLES
+    const unsigned long long tf0 = trace ? MR_CLOCK() : 0ull;
+#endif
+    const T mu = this->mu;
+    const T tau = mr_max(T(0.99), T(1) - mu);
+    T dz[NZS];
+    for (int i = 0; i < NZS; ++i) dz[i] = T(0);
+    fwd_recursion<false>(dz);
 #if MR_PHASE_CYCLES
     const unsigned long long tf1 = trace ? MR_CLOCK() : 0ull;
 #endif
@@ -1964,36 +1984,40 @@ struct WaveSolver {
     const unsigned junk = (unsigned)(CSF::SJUNK * WL + ln);
     // one stage's operands: P_{k+1} row li, c_k, A_k column li (J column li, vehicle rows), B's J
     // columns, K_k column li, Q_uu's factor, g_x[li], g_u
+    // the shared operands (c_k, B's J columns, Q_uu's factor, g_u) are loaded one word per lane and
+    // broadcast by v_readlane at use: one vector load each instead of one per word
+    const int l12 = ln < 12 ? ln : 0;
     struct Ops {
-      T prow[NX], c[NX], acol[6], jb[12], kcol[NU], lq[6], gx, gu[NU];
+      T prow[NX], acol[6], kcol[NU], gx, c_w, jb_w, lq_w, gu_w;
     };
     auto ld = [&](int k, Ops& o) {
       const MR_GLOBAL T* Rk = R(k);
       const MR_GLOBAL T* Rn = R(k + 1);
       for (int l = 0; l < NX; ++l) o.prow[l] = Rn[RCF::P + pidx(li, l)];
-      for (int l = 0; l < NX; ++l) o.c[l] = cb[(CSF::SC + l) * WL + k];
       for (int j = 0; j < 6; ++j) o.acol[j] = Rk[RCF::J + j * 8 + (li < 6 ? li : 0)];
-      for (int j = 0; j < 6; ++j) { o.jb[2 * j] = Rk[RCF::J + j * 8 + 6]; o.jb[2 * j + 1] = Rk[RCF::J + j * 8 + 7]; }
       for (int a = 0; a < NU; ++a) o.kcol[a] = Rk[RCF::K + a * NX + li];
-      for (int q = 0; q < 6; ++q) o.lq[q] = Rk[RCF::LQ + q];
       o.gx = cb[(CSF::SG + li) * WL + k];
-      for (int a = 0; a < NU; ++a) o.gu[a] = cb[(CSF::SG + NX + a) * WL + k];
+      o.c_w = cb[(CSF::SC + li) * WL + k];                        // lane l: c_k[l]
+      o.jb_w = Rk[RCF::J + (l12 >> 1) * 8 + 6 + (l12 & 1)];      // lane 2j + a: J[j][6 + a]
+      o.lq_w = Rk[RCF::LQ + (ln < 6 ? ln : 0)];                  // lane q: Q_uu factor word q
+      o.gu_w = cb[(CSF::SG + NX + (ln < NU ? ln : 0)) * WL + k];  // lane a: g_u[a]
     };
     T pv = cb[(CSF::SG + li) * WL + N];
     wb.st(pv, 0u, row ? (unsigned)((CSF::SPV + li) * WL + N) : junk);
-    Ops nx;
-    if (N > 0) ld(N - 1, nx);
-    for (int k = N - 1; k >= 0; --k) {
-      const Ops o = nx;
-      if (k > 0) ld(k - 1, nx);
+    auto step = [&](int k, const Ops& o) {
+      T c[NX], jb[12], lq[6], gu[NU];
+      wgather<T, NX>(w, o.c_w, c);
+      wgather<T, 12>(w, o.jb_w, jb);
+      wgather<T, 6>(w, o.lq_w, lq);
+      wgather<T, NU>(w, o.gu_w, gu);
       T pcl = pv;
-      for (int l = 0; l < NX; ++l) pcl += o.prow[l] * o.c[l];
+      for (int l = 0; l < NX; ++l) pcl += o.prow[l] * c[l];
       T pc[NX];
       wgather<T, NX>(w, pcl, pc);
       // r = B^T pc + g_u (mr_solver.h apply_Bt), every lane
-      T r[NU] = {pc[7] + o.gu[0], pc[8] + o.gu[1], pc[6] + o.gu[2]};
+      T r[NU] = {pc[7] + gu[0], pc[8] + gu[1], pc[6] + gu[2]};
       if (k == 0) { r[0] += pc[9]; r[1] += pc[10]; }
-      for (int j = 0; j < 6; ++j) { r[0] += o.jb[2 * j] * pc[j]; r[1] += o.jb[2 * j + 1] * pc[j]; }
+      for (int j = 0; j < 6; ++j) { r[0] += jb[2 * j] * pc[j]; r[1] += jb[2 * j + 1] * pc[j]; }
       // (A^T pc)[li] (mr_solver.h apply_At)
       T at;
       if (li < 6) {
@@ -2005,96 +2029,66 @@ struct WaveSolver {
       pv = o.gx + at + o.kcol[0] * r[0] + o.kcol[1] * r[1] + o.kcol[2] * r[2];
       wb.st(pv, 0u, row ? (unsigned)((CSF::SPV + li) * WL + k) : junk);
       // k_k = -Q_uu^-1 r with Q_uu = L L^T (L10, L20, L21, reciprocal pivots from the Riccati sweep)
-      const T Lf[6] = {T(0), o.lq[0], T(0), o.lq[1], o.lq[2], T(0)};
-      const T iv[3] = {o.lq[3], o.lq[4], o.lq[5]};
+      const T Lf[6] = {T(0), lq[0], T(0), lq[1], lq[2], T(0)};
+      const T iv[3] = {lq[3], lq[4], lq[5]};
       T kf[NU] = {-r[0], -r[1], -r[2]};
       lsolve3r(Lf, iv, kf);
       ltsolve3r(Lf, iv, kf);
       const T kv = ln == 0 ? kf[0] : (ln == 1 ? kf[1] : kf[2]);
       wb.st(kv, 0u, ln < NU ? (unsigned)((CSF::SK0 + ln) * WL + k) : junk);
+    };
+    // operands three stages ahead, four rotating sets (unrolled by four: compile-time set roles, no
+    // register copies of in-flight loads; one stage ahead left every stage waiting out a memory round
+    // trip); a prefetch past stage 0 re-reads stage 0 (unconditional loads, exact waits)
+    if (N > 0) {
+      auto kc = [](int k) { return k > 0 ? k : 0; };
+      Ops b0, b1, b2, b3;
+      ld(N - 1, b0);
+      ld(kc(N - 2), b1);
+      ld(kc(N - 3), b2);
+      for (int k = N - 1;; k -= 4) {
+        ld(kc(k - 3), b3);
+        step(k, b0);
+        if (k == 0) break;
+        ld(kc(k - 4), b0);
+        step(k - 1, b1);
+        if (k == 1) break;
+        ld(kc(k - 5), b1);
+        step(k - 2, b2);
+        if (k == 2) break;
+        ld(kc(k - 6), b2);
+        step(k - 3, b3);
+        if (k == 3) break;
+      }
     }
     wsync(w);
   }
-  // the SOC direction (mr_solver.h Solver::forward with soc set): SDZ, SDS, SDLAM, SDY, SDNU.
-  // The recursion du_k = k_k + K_k dx_k, dx_{k+1} = A_k dx_k + B_k du_k + c_k on lanes 0..10 (lane i:
-  // component i of dx, the others' by v_readlane; every lane forms du from K_k and k_k as uniform
-  // loads), dx_k to SDZ[0..10] and du_k to SDZ[11..13] of stage k; then stage-parallel the costate step
-  // dnu_k = pv_k + P_k dx_k, the rows' steps and the step limits.
+  // the SOC direction (mr_solver.h Solver::forward with soc set): SDZ, SDS, SDLAM, SDY, SDNU.  The recursion
+  // is the Newton direction's (fwd_recursion, its lane groups and prefetch) with the SOC's feed-forward,
+  // constant and costate vector; then stage-parallel the rows' steps and the step limits.
   MR_SWEEP void forward_soc(T& ap, T& ad) {
     MR_UNIFORM_P();
     MR_ASSUME_LDS_STATE();
     const T tau = mr_max(T(0.99), T(1) - mu);
     const int N = wu(w, this->N);
-    const MR_GLOBAL T* cb = rc + (int64_t)RC_STRIDE * WL;
-    {
-      const WBuf<T> wb(rc + (int64_t)RC_STRIDE * WL, (unsigned)CSF::NF * WL);
-      const bool row = ln < NX;
-      const int li = row ? ln : 0;
-      const unsigned junk = (unsigned)(CSF::SJUNK * WL + ln);
-      struct Ops {
-        T K[NU * NX], kf[NU], arow[6], brow[2], c;
-      };
-      auto ld = [&](int k, Ops& o) {
-        const MR_GLOBAL T* Rk = R(k);
-        for (int q = 0; q < NU * NX; ++q) o.K[q] = Rk[RCF::K + q];
-        for (int a = 0; a < NU; ++a) o.kf[a] = cb[(CSF::SK0 + a) * WL + k];
-        const int r6 = li < 6 ? li : 0;
-        for (int j = 0; j < 6; ++j) o.arow[j] = Rk[RCF::J + r6 * 8 + j];
-        o.brow[0] = Rk[RCF::J + r6 * 8 + 6];
-        o.brow[1] = Rk[RCF::J + r6 * 8 + 7];
-        o.c = cb[(CSF::SC + li) * WL + k];
-      };
-      T dx = T(0);
-      wb.st(dx, 0u, row ? (unsigned)((CSF::SDZ + li) * WL + 0) : junk);
-      Ops nx;
-      if (N > 0) ld(0, nx);
-      for (int k = 0; k < N; ++k) {
-        const Ops o = nx;
-        if (k + 1 < N) ld(k + 1, nx);
-        T dxa[NX];
-        wgather<T, NX>(w, dx, dxa);
-        T du[NU];
-        for (int a = 0; a < NU; ++a) {
-          T v = o.kf[a];
-          for (int j = 0; j < NX; ++j) v += o.K[a * NX + j] * dxa[j];
-          du[a] = v;
-        }
-        const T duv = ln == 0 ? du[0] : (ln == 1 ? du[1] : du[2]);
-        wb.st(duv, 0u, ln < NU ? (unsigned)((CSF::SDZ + NX + ln) * WL + k) : junk);
-        // row li of A dx + B du (mr_solver.h apply_A / apply_B)
-        T v;
-        if (li < 6) {
-          v = o.brow[0] * du[0] + o.brow[1] * du[1];
-          for (int j = 0; j < 6; ++j) v += o.arow[j] * dxa[j];
-        } else if (li == 6) {
-          v = dxa[6] + du[2];
-        } else if (li == 7) {
-          v = du[0];
-        } else if (li == 8) {
-          v = du[1];
-        } else {
-          v = k == 0 ? (li == 9 ? du[0] : du[1]) : (li == 9 ? dxa[9] : dxa[10]);
-        }
-        dx = v + o.c;
-        wb.st(dx, 0u, row ? (unsigned)((CSF::SDZ + li) * WL + k + 1) : junk);
-      }
-    }
-    wsync(w);
+    T dzr[NZS];
+    for (int i = 0; i < NZS; ++i) dzr[i] = T(0);
+#if MR_PHASE_CYCLES
+    const unsigned long long tc0 = trace ? MR_CLOCK() : 0ull;
+#endif
+    fwd_recursion<true>(dzr);
+    wsync(w);  // SDNU (the recursion's costate steps) visible
+#if MR_PHASE_CYCLES
+    if (trace) tsub[2] += MR_CLOCK() - tc0;
+    const unsigned long long tp0 = trace ? MR_CLOCK() : 0ull;
+#endif
     T ap_l = T(1), ad_l = T(1), g_l = T(0);
     if (own()) {
       const int k = ln;
       const MR_GLOBAL T* Rk = R(k);
       T dz[NZS];
-      for (int i = 0; i < NZS; ++i) dz[i] = T(0);
-      for (int i = 0; i < NX; ++i) dz[i] = Cf(CSF::SDZ + i);
-      if (k < N)
-        for (int a = 0; a < NU; ++a) dz[NX + a] = Cf(CSF::SDZ + NX + a);
-      if (k > 0 || !MR_KKT_RESTATED)  // the costate (multiplier) step of x_k's rows (k = 0: the initial-state rows')
-        for (int i = 0; i < NX; ++i) {
-          T v = Cf(CSF::SPV + i);
-          for (int l = 0; l < NX; ++l) v += Rk[RCF::P + pidx(i, l)] * dz[l];
-          Cf(CSF::SDNU + i) = v;
-        }
+      for (int i = 0; i < NZS; ++i) dz[i] = dzr[i];
+      (void)Rk;
       T z[NZS];
       load_z(cur, z);
       Err<T> e;
@@ -2122,6 +2116,9 @@ struct WaveSolver {
     ap = wmin(w, ap_l);
     ad = wmin(w, ad_l);
     wsync(w);
+#if MR_PHASE_CYCLES
+    if (trace) tsub[3] += MR_CLOCK() - tp0;
+#endif
   }
   // the accepted correction becomes the iteration's direction; returns its dual step size
   MR_SWEEP T soc_commit() {

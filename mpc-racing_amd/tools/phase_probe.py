@@ -40,7 +40,7 @@ def one(name, b, i, cap=520):
     tr = out["trace"].cpu().numpy()
     it = int(out["iters"][0])
     row = dict(zip(NAMES, tr[-1].tolist()))
-    row.update(dict(zip(["fwd_seq", "fwd_par", "eval_stage", "eval_reduce", "fact_failed_cycles", "n_fact_failed",
+    row.update(dict(zip(["fwd_seq", "fwd_par", "socf_chain", "socf_par", "fact_failed_cycles", "n_fact_failed",
                         "soc_backward", "soc_forward"], tr[-2][:8].tolist())))
     row.update(instance=i, iters=it, status=int(out["status"][0]), wall_ms=1e3 * min(lat),
                cycles_per_iter=row["total"] / max(it, 1))
@@ -68,7 +68,7 @@ def main():
             tr = o["trace"].cpu().numpy()
             it_i = int(o["iters"][i])
             row = dict(zip(NAMES, tr[-1].tolist()))
-            row.update(dict(zip(["fwd_seq", "fwd_par", "eval_stage", "eval_reduce", "fact_failed_cycles",
+            row.update(dict(zip(["fwd_seq", "fwd_par", "socf_chain", "socf_par", "fact_failed_cycles",
                                  "n_fact_failed", "soc_backward", "soc_forward"], tr[-2][:8].tolist())))
             row.update(instance=i, iters=it_i, status=int(o["status"][i]), in_batch=True,
                        cycles_per_iter=row["total"] / max(it_i, 1))
