@@ -1988,7 +1988,7 @@ struct WaveSolver {
     // broadcast by v_readlane at use: one vector load each instead of one per word
     const int l12 = ln < 12 ? ln : 0;
     struct Ops {
-      T prow[NX], acol[6], kcol[NU], gx, c_w, jb_w, lq_w, gu_w;
+      T prow[NX], acol[6], kcol[NU], gx, c_w, jb_w, gu_w;
     };
     auto ld = [&](int k, Ops& o) {
       const MR_GLOBAL T* Rk = R(k);
@@ -1999,16 +1999,14 @@ struct WaveSolver {
       o.gx = cb[(CSF::SG + li) * WL + k];
       o.c_w = cb[(CSF::SC + li) * WL + k];                        // lane l: c_k[l]
       o.jb_w = Rk[RCF::J + (l12 >> 1) * 8 + 6 + (l12 & 1)];      // lane 2j + a: J[j][6 + a]
-      o.lq_w = Rk[RCF::LQ + (ln < 6 ? ln : 0)];                  // lane q: Q_uu factor word q
       o.gu_w = cb[(CSF::SG + NX + (ln < NU ? ln : 0)) * WL + k];  // lane a: g_u[a]
     };
     T pv = cb[(CSF::SG + li) * WL + N];
     wb.st(pv, 0u, row ? (unsigned)((CSF::SPV + li) * WL + N) : junk);
     auto step = [&](int k, const Ops& o) {
-      T c[NX], jb[12], lq[6], gu[NU];
+      T c[NX], jb[12], gu[NU];
       wgather<T, NX>(w, o.c_w, c);
       wgather<T, 12>(w, o.jb_w, jb);
-      wgather<T, 6>(w, o.lq_w, lq);
       wgather<T, NU>(w, o.gu_w, gu);
       T pcl = pv;
       for (int l = 0; l < NX; ++l) pcl += o.prow[l] * c[l];
@@ -2028,14 +2026,9 @@ struct WaveSolver {
       }
       pv = o.gx + at + o.kcol[0] * r[0] + o.kcol[1] * r[1] + o.kcol[2] * r[2];
       wb.st(pv, 0u, row ? (unsigned)((CSF::SPV + li) * WL + k) : junk);
-      // k_k = -Q_uu^-1 r with Q_uu = L L^T (L10, L20, L21, reciprocal pivots from the Riccati sweep)
-      const T Lf[6] = {T(0), lq[0], T(0), lq[1], lq[2], T(0)};
-      const T iv[3] = {lq[3], lq[4], lq[5]};
-      T kf[NU] = {-r[0], -r[1], -r[2]};
-      lsolve3r(Lf, iv, kf);
-      ltsolve3r(Lf, iv, kf);
-      const T kv = ln == 0 ? kf[0] : (ln == 1 ? kf[1] : kf[2]);
-      wb.st(kv, 0u, ln < NU ? (unsigned)((CSF::SK0 + ln) * WL + k) : junk);
+      // r to SK0 (lanes 0..2); the feed-forward k_k = -Q_uu^-1 r is formed stage-parallel afterwards
+      const T rv = ln == 0 ? r[0] : (ln == 1 ? r[1] : r[2]);
+      wb.st(rv, 0u, ln < NU ? (unsigned)((CSF::SK0 + ln) * WL + k) : junk);
     };
     // operands three stages ahead, four rotating sets (unrolled by four: compile-time set roles, no
     // register copies of in-flight loads; one stage ahead left every stage waiting out a memory round
@@ -2060,6 +2053,16 @@ struct WaveSolver {
         step(k - 3, b3);
         if (k == 3) break;
       }
+    }
+    wsync(w);
+    if (own() && ln < N) {  // k_k = -Q_uu^-1 r (L10, L20, L21 and the reciprocal pivots from the Riccati sweep)
+      const MR_GLOBAL T* Rk = R(ln);
+      const T Lf[6] = {T(0), Rk[RCF::LQ + 0], T(0), Rk[RCF::LQ + 1], Rk[RCF::LQ + 2], T(0)};
+      const T iv[3] = {Rk[RCF::LQ + 3], Rk[RCF::LQ + 4], Rk[RCF::LQ + 5]};
+      T kf[NU] = {-Cf(CSF::SK0 + 0), -Cf(CSF::SK0 + 1), -Cf(CSF::SK0 + 2)};
+      lsolve3r(Lf, iv, kf);
+      ltsolve3r(Lf, iv, kf);
+      for (int a = 0; a < NU; ++a) Cf(CSF::SK0 + a) = kf[a];
     }
     wsync(w);
   }
