@@ -25,7 +25,7 @@ struct mr_handle {
   void* params_dev;  // ProbParams<T> of the handle's precision (device copy, set by upload_params)
   void* ws;
   size_t ws_bytes;
-  int* order;  // [max_batch] workgroup -> instance (mr_order_kernel)
+  int* order;  // [2][max_batch] workgroup -> instance (mr_order_kernel), then mr_order_hint_kernel's buckets
   int32_t* last_iters;  // [max_batch] the previous solve's iterations (dispatch_order 2's default hint)
   int last_B;           // batch size of that solve (0: none yet)
   TyreCoef<double> tf, tr;
@@ -192,21 +192,31 @@ __global__ __launch_bounds__(kOrderThreads) void mr_order_kernel(const double* s
 }
 
 // dispatch_order = 2: workgroups take instances in decreasing order_hint (longest expected first), e.g.
-// the previous MPC tick's iteration counts.  One workgroup: bucket histogram (hint clamped to
-// 0..kHintBuckets-1) in LDS, a scan from the largest bucket down, then an atomic scatter (the order within
-// a bucket is arbitrary; results do not depend on the order).  A hint that says nothing (every instance in
-// one bucket, e.g. all zero) gives instance order: no model-specific guess.
+// the previous MPC tick's iteration counts.  One workgroup: each hint is read ONCE into a bucket index
+// (clamped to 0..kHintBuckets-1, kept in `bucket`, the second half of the handle's order buffer), a bucket
+// histogram in LDS, a scan from the largest bucket down, then an atomic scatter from the stored buckets (the
+// order within a bucket is arbitrary; results do not depend on the order).  Reading the hint once keeps
+// `order` a permutation even if the hint buffer changes under the kernel (a caller's unordered stream); the
+// scatter index is clamped to the batch besides.  A hint that says nothing (every instance in one bucket,
+// e.g. all zero) gives instance order: no model-specific guess.
 constexpr int kHintBuckets = kOrderThreads;
 __device__ __forceinline__ int hint_bucket(int h) { return h < 0 ? 0 : (h >= kHintBuckets ? kHintBuckets - 1 : h); }
-__global__ __launch_bounds__(kOrderThreads) void mr_order_hint_kernel(const int32_t* hint, int B, int* order) {
+__global__ __launch_bounds__(kOrderThreads) void mr_order_hint_kernel(const int32_t* hint, int B, int* order,
+                                                                       int* bucket) {
   __shared__ int cnt[kHintBuckets];
   __shared__ int scan[kOrderThreads];
+  __shared__ int b0;
   const int t = threadIdx.x;
   cnt[t] = 0;
   __syncthreads();
-  for (int i = t; i < B; i += kOrderThreads) atomicAdd(&cnt[hint_bucket(hint[i])], 1);
+  for (int i = t; i < B; i += kOrderThreads) {
+    const int b = hint_bucket(hint[i]);
+    bucket[i] = b;
+    if (i == 0) b0 = b;
+    atomicAdd(&cnt[b], 1);
+  }
   __syncthreads();
-  if (cnt[hint_bucket(hint[0])] == B) {  // uniform hint (block-uniform branch): instance order
+  if (cnt[b0] == B) {  // uniform hint (block-uniform branch): instance order
     for (int i = t; i < B; i += kOrderThreads) order[i] = i;
     return;
   }
@@ -215,7 +225,10 @@ __global__ __launch_bounds__(kOrderThreads) void mr_order_hint_kernel(const int3
   const int incl = order_scan(scan, t, c);
   cnt[r] = incl - c;  // first slot of bucket r
   __syncthreads();
-  for (int i = t; i < B; i += kOrderThreads) order[atomicAdd(&cnt[hint_bucket(hint[i])], 1)] = i;
+  for (int i = t; i < B; i += kOrderThreads) {
+    const int slot = atomicAdd(&cnt[bucket[i]], 1);  // this thread's own bucket store: no fence needed
+    if (slot < B) order[slot] = i;
+  }
 }
 
 static size_t ws_bytes_per_instance(const mr_config& c) {
@@ -249,7 +262,8 @@ static int launch(mr_handle* h, int B, const mr_inputs* in, mr_outputs* out, hip
     // previous tick), else instance order -- no model-specific guess
     const int32_t* hint = in->order_hint ? in->order_hint : (h->last_B == B ? h->last_iters : nullptr);
     if (hint) {
-      hipLaunchKernelGGL(mr_order_hint_kernel, dim3(1), dim3(kOrderThreads), 0, st, hint, B, h->order);
+      hipLaunchKernelGGL(mr_order_hint_kernel, dim3(1), dim3(kOrderThreads), 0, st, hint, B, h->order,
+                         h->order + h->cfg.max_batch);
       HIP_TRY(hipGetLastError());
       order = h->order;
     }
@@ -508,7 +522,7 @@ int mr_create(mr_handle** out, const mr_config* cfg) {
   h->last_iters = nullptr;
   h->last_B = 0;
   hipError_t e = hipMalloc(&h->ws, h->ws_bytes);
-  if (e == hipSuccess) e = hipMalloc((void**)&h->order, sizeof(int) * (size_t)cfg->max_batch);
+  if (e == hipSuccess) e = hipMalloc((void**)&h->order, 2 * sizeof(int) * (size_t)cfg->max_batch);  // + the hint buckets
   if (e == hipSuccess) e = hipMalloc((void**)&h->last_iters, sizeof(int32_t) * (size_t)cfg->max_batch);
   if (e == hipSuccess) e = hipMalloc(&h->params_dev, sizeof(ProbParams<double>));
   if (e != hipSuccess) {

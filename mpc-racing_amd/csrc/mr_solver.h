@@ -91,7 +91,9 @@ struct WF {
     CDVN = CDVP + 6, CSW = CDVN + 6, CGW0 = CSW + 6, CGW1 = CGW0 + 6,
     // the restoration phase's entry point (slacks, bound duals: the bound-multiplier update on return)
     // and IPOPT's stored acceptable iterate (returned if the line search fails at an almost feasible point)
-    RS0 = CGW1 + 6, RLAM = RS0 + NI, AZ = RLAM + NI, NF = AZ + NZS
+    RS0 = CGW1 + 6, RLAM = RS0 + NI, AZ = RLAM + NI,
+    ASL = AZ + NZS, ALAM = ASL + NI, AY = ALAM + NI,  // its slacks and multipliers
+    NF = AY + NI
   };
 };
 
@@ -817,7 +819,7 @@ struct Solver {
   int trace_cap = 0;
   // the dynamics rows' multipliers nu_k (x_k = F(x_{k-1}, u_{k-1}), k >= 1) and their watchdog copy, fp64
   // in both precisions (correction form: eval_sweep)
-  double nub[64][NX], wnub[64][NX];
+  double nub[64][NX], wnub[64][NX], anub[64][NX];  // (anub: the stored acceptable point's)
 
   MR_HD Solver(const ProbParams<T>& P_, const Inst<T>& I_, WS<T> W_) : P(P_), I(I_), W(W_), N(P_.N) {}
 
@@ -1997,14 +1999,31 @@ struct Solver {
     }
   }
   double acc_kkt = 0.0, acc_obj = 0.0, acc_viol = 0.0;  // the stored acceptable point's measures
-  MR_HD void acc_save() {  // IPOPT's backup acceptable iterate (primal part: what the solve returns)
-    for (int k = 0; k <= N; ++k)
+  // IPOPT's backup acceptable iterate (RestoreAcceptablePoint): the whole iterate -- primal part, slacks,
+  // bound duals, row multipliers y_d and the dynamics multipliers -- so a solve that returns it returns
+  // multipliers that belong to it
+  MR_HD void acc_save() {
+    for (int k = 0; k <= N; ++k) {
       for (int i = 0; i < NZS; ++i) W(k, WF::AZ + i) = W(k, zf(cur) + i);
+      for (int j = 0; j < NI; ++j) {
+        W(k, WF::ASL + j) = W(k, sf(cur) + j);
+        W(k, WF::ALAM + j) = W(k, WF::LAM + j);
+        W(k, WF::AY + j) = W(k, WF::Y + j);
+      }
+      for (int i = 0; i < NX; ++i) anub[k][i] = nub[k][i];
+    }
     have_acc = true;
   }
   MR_HD void acc_restore() {
-    for (int k = 0; k <= N; ++k)
+    for (int k = 0; k <= N; ++k) {
       for (int i = 0; i < NZS; ++i) W(k, zf(cur) + i) = W(k, WF::AZ + i);
+      for (int j = 0; j < NI; ++j) {
+        W(k, sf(cur) + j) = W(k, WF::ASL + j);
+        W(k, WF::LAM + j) = W(k, WF::ALAM + j);
+        W(k, WF::Y + j) = W(k, WF::AY + j);
+      }
+      for (int i = 0; i < NX; ++i) nub[k][i] = anub[k][i];
+    }
   }
 
   // ---------------- the restoration phase (IPOPT's l1 restoration, W&B 2006 sec. 3.3) ----------------

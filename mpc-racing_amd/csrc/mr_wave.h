@@ -130,7 +130,8 @@ struct CSF {
     // costate p, feed-forward k); the restoration entry point; IPOPT's stored acceptable iterate
     SC = WDY + NI, SR = SC + NX, SG = SR + NI, SPV = SG + NZ, SK0 = SPV + NX, SDZ = SK0 + NU, SDS = SDZ + NZS,
     SDLAM = SDS + NI, SDY = SDLAM + NI, SDNU = SDY + NI, RS0 = SDNU + NX, RLAM = RS0 + NI, AZ = RLAM + NI,
-    RP = AZ + NZS, RN = RP + NI, RVP = RN + NI, RVN = RVP + NI, RDP = RVN + NI, RDN = RDP + NI, RDVP = RDN + NI,
+    ASL = AZ + NZS, ALAM = ASL + NI, AY = ALAM + NI,  // the stored acceptable point's slacks and multipliers
+    RP = AY + NI, RN = RP + NI, RVP = RN + NI, RVN = RVP + NI, RDP = RVN + NI, RDN = RDP + NI, RDVP = RDN + NI,
     RDVN = RDVP + NI, RY = RDVN + NI, RDY = RY + NI, RZ = RDY + NI,
     CP = RZ + NZS, CN = CP + 6, CVP = CN + 6, CVN = CVP + 6, CDP = CVN + 6, CDN = CDP + 6, CDVP = CDN + 6,
     CDVN = CDVP + 6, CSW = CDVN + 6, CGW0 = CSW + 6, CGW1 = CGW0 + 6,
@@ -138,12 +139,12 @@ struct CSF {
     NF = SJUNK + 1
   };
 };
-// The dynamics rows' multipliers nu (and their watchdog snapshot) in fp64 whatever the solve precision,
-// [2][NX][64] doubles after the cold fields: eval_sweep forms the stationarity residual and the
+// The dynamics rows' multipliers nu (and their watchdog and acceptable-point snapshots) in fp64 whatever
+// the solve precision, [3][NX][64] doubles after the cold fields: eval_sweep forms the stationarity residual and the
 // Riccati right-hand side from them in fp64 (the correction form, see there).
 constexpr int64_t WS_NU_OFF = (int64_t)SSF::NF * WL + (int64_t)RC_STRIDE * WL + (int64_t)CSF::NF * WL;  // words
 template <typename T>
-MR_HD constexpr int64_t ws_words() { return WS_NU_OFF + 2 * NX * WL * (int64_t)(sizeof(double) / sizeof(T)); }
+MR_HD constexpr int64_t ws_words() { return WS_NU_OFF + 3 * NX * WL * (int64_t)(sizeof(double) / sizeof(T)); }
 
 // Wave-uniform state of the watchdog and the restoration phase: one copy per wavefront next to the
 // line-search filter (LDS on the device), every lane writing the same values -- not in the per-lane
@@ -263,6 +264,7 @@ constexpr int SS_WORDS = SSF::NF * WL;
 
 template <typename T, int MODEL, bool SSL = false>
 struct WaveSolver {
+  static constexpr int kModel = MODEL;
   // problem constants: device memory read through a constant-address-space pointer made wave-uniform
   // in every method (MR_UNIFORM_P), so they are scalar loads into SGPRs, not VGPRs
   const MR_CONST ProbParams<T>& P;
@@ -311,6 +313,7 @@ struct WaveSolver {
   MR_HD MR_GLOBAL double* nub() const { return (MR_GLOBAL double*)(rc + (int64_t)(RC_STRIDE + CSF::NF) * WL); }
   MR_HD MR_GLOBAL double& NUd(int i) const { return nub()[i * WL + ln]; }
   MR_HD MR_GLOBAL double& WNUd(int i) const { return nub()[(NX + i) * WL + ln]; }
+  MR_HD MR_GLOBAL double& ANUd(int i) const { return nub()[(2 * NX + i) * WL + ln]; }  // acceptable-point copy
   MR_HD auto& fth(int i) const { return filt[i]; }
   MR_HD auto& fph(int i) const { return filt[FMAX + i]; }
   MR_HD MR_GLOBAL T* R(int k) const { return rc + (int64_t)k * RC_STRIDE; }
@@ -2351,19 +2354,35 @@ struct WaveSolver {
     C->resto = 0;
     wsync(w);
   }
-  // IPOPT's backup acceptable iterate: stored when the current point is acceptable (primal part: what
-  // the solve returns), returned if the line search later fails at an almost feasible point
+  // IPOPT's backup acceptable iterate (RestoreAcceptablePoint): stored when the current point is acceptable
+  // -- the whole iterate, primal part, slacks and every multiplier (bound duals, row multipliers y_d, the
+  // fp64 dynamics multipliers) -- and returned whole if the line search later fails at an almost feasible
+  // point or the fp32 stall exit fires, so the exported lam_g belongs to the returned X / U
   MR_SWEEP void acc_save() {
     MR_ASSUME_LDS_STATE();
-    if (own())
+    if (own()) {
       for (int i = 0; i < NZS; ++i) Cf(CSF::AZ + i) = S(zf(cur) + i);
+      for (int j = 0; j < NI; ++j) {
+        Cf(CSF::ASL + j) = S(sf(cur) + j);
+        Cf(CSF::ALAM + j) = S(SSF::LAM + j);
+        Cf(CSF::AY + j) = S(SSF::Y + j);
+      }
+      for (int i = 0; i < NX; ++i) ANUd(i) = NUd(i);
+    }
     cw()->have_acc = 1;
     wsync(w);
   }
   MR_SWEEP void acc_restore() {
     MR_ASSUME_LDS_STATE();
-    if (own())
+    if (own()) {
       for (int i = 0; i < NZS; ++i) S(zf(cur) + i) = Cf(CSF::AZ + i);
+      for (int j = 0; j < NI; ++j) {
+        S(sf(cur) + j) = Cf(CSF::ASL + j);
+        S(SSF::LAM + j) = Cf(CSF::ALAM + j);
+        S(SSF::Y + j) = Cf(CSF::AY + j);
+      }
+      for (int i = 0; i < NX; ++i) NUd(i) = ANUd(i);
+    }
     wsync(w);
   }
 
@@ -2799,11 +2818,14 @@ MR_HD void solve_instance_wave(const MR_CONST ProbParams<T>& P, const mr_inputs&
 
 // The reference's dual (control/MPC.py:171: sol.value(opti.lam_g)) from the stage-wise multipliers, in
 // Opti row order (include/mpcracing.h lam_g).  Derivation: the solver's Lagrangian is
-// sc*f + sum nu_{k+1}.(F(x_k, u_k) - x_{k+1}) - sum lam.d, Opti's is f + lam_g.g with g = X_i - f(X_{i-1},
-// U_{i-1}), so the dynamics rows are -nu/sc; every inequality row of the reference is a row of the
-// restatement (Delta-S = the u[2] box, rate rows via the previous-control state p, the i = 0 wrap rows via
-// the frozen copy w at k = N-1), lam_g = (lam_upper - lam_lower)/sc; S_0 and X_{:,0} follow from the
-// reference's stationarity in those variables: lam_S0 = lam_ds(1), lam_X0 = A_0^T lam_dyn(1).
+// sc*f + sum nu_{k+1}.(F(x_k, u_k) - x_{k+1}) + sum y_d (d - s), Opti's is f + lam_g.g with g = X_i -
+// f(X_{i-1}, U_{i-1}), so the dynamics rows are -nu/sc; every inequality row of the reference is an IPOPT row
+// of the restatement (Delta-S = the u[2] box, rate rows via the previous-control state p, the i = 0 wrap rows
+// via the frozen copy w at k = N-1) and its lam_g is that row's own multiplier y_d / sc -- IPOPT's y_d, which
+// CasADi returns as lam_g (positive at an active upper bound; the box rows' lower halves carry -v_L), not the
+// slack bound duals v_U - v_L, which equal it only where the slack stationarity -y_d - v_L + v_U vanishes;
+// S_0 and X_{:,0} follow from the reference's stationarity in those variables: lam_S0 = lam_ds(1),
+// lam_X0 = A_0^T lam_dyn(1).
 template <typename Solver>
 MR_HD void write_lam_g(Solver& S, const mr_outputs& out, int64_t B, int64_t i, int N, Wv w) {
   typedef decltype(S.mu) T;
@@ -2811,39 +2833,42 @@ MR_HD void write_lam_g(Solver& S, const mr_outputs& out, int64_t B, int64_t i, i
   const double isc = 1.0 / (double)S.sc;
   const int rows = 13 * N + 9;
   auto put = [&](int row, double v) { out.lam_g[(int64_t)row * B + i] = v; };
-  auto lam = [&](int j) { return (double)S.S(SSF::LAM + j); };
+  auto yd = [&](int j) { return (double)S.S(SSF::Y + j); };  // the row multiplier of slot j (a y-slot)
   double nu1[NX];
   for (int q = 0; q < NX; ++q) nu1[q] = wshfl(w, S.own() ? S.NUd(q) : 0.0, 1);
-  const double ds1 = wshfl(w, S.own() && k < N ? (lam(5) - lam(4)) * isc : 0.0, 0);
+  const double ds1 = wshfl(w, S.own() && k < N ? yd(4) * isc : 0.0, 0);
   if (k >= 1 && k <= N)
     for (int q = 0; q < 6; ++q) put(7 + 7 * (k - 1) + q, -S.NUd(q) * isc);
   if (k < N) {
-    put(7 + 7 * k + 6, (lam(5) - lam(4)) * isc);  // Delta-S row of i = k + 1 (u[2] box of stage k)
+    put(7 + 7 * k + 6, yd(4) * isc);  // Delta-S row of i = k + 1 (u[2] box of stage k)
     const int b = 7 + 7 * N + 6 * k;
-    put(b + 0, lam(1) * isc);    // U[0,k] < d_max
-    put(b + 1, -lam(0) * isc);   // U[0,k] > min_throttle
-    put(b + 2, lam(3) * isc);    // U[1,k] < max_steer
-    put(b + 3, -lam(2) * isc);   // U[1,k] > min_steer
+    put(b + 0, yd(1) * isc);  // U[0,k] < d_max
+    put(b + 1, yd(0) * isc);  // U[0,k] > min_throttle
+    put(b + 2, yd(3) * isc);  // U[1,k] < max_steer
+    put(b + 3, yd(2) * isc);  // U[1,k] > min_steer
     if (k >= 1) {
-      put(b + 4, (lam(7) - lam(6)) * isc);
-      put(b + 5, (lam(9) - lam(8)) * isc);
+      put(b + 4, yd(6) * isc);
+      put(b + 5, yd(8) * isc);
     }
     if (k == N - 1) {  // i = 0 rate rows U[:,0] - U[:,N-1]: the frozen-copy rows at stage N-1
       const int b0 = 7 + 7 * N;
-      put(b0 + 4, N >= 2 ? (lam(11) - lam(10)) * isc : 0.0);
-      put(b0 + 5, N >= 2 ? (lam(13) - lam(12)) * isc : 0.0);
+      put(b0 + 4, N >= 2 ? yd(10) * isc : 0.0);
+      put(b0 + 5, N >= 2 ? yd(12) * isc : 0.0);
     }
   }
   if (k == 0) {
     put(0, ds1);  // S_0 == s0
-    MR_GLOBAL T* R0 = S.R(0);
-    T J[48];
+    // A_0 at the returned point (after an acceptable-point restore the record holds the abandoned one's)
+    T z[NZS], J[48], Hd[36], fx[6], nz[NX];
+    S.load_z(S.cur, z);
+    for (int q = 0; q < NX; ++q) nz[q] = T(0);
+    const ProbParams<T>& Pg = *(const ProbParams<T>*)wu_ptr(&S.P);
+    Dyn<T, Solver::kModel>::fjh(Pg, z, z + NX, nz, fx, J, Hd);
     double at[NX];
-    for (int q = 0; q < 48; ++q) J[q] = R0[RCF::J + q];
     apply_At(J, 0, nu1, at);
     for (int q = 0; q < 6; ++q) put(1 + q, -at[q] * isc);  // X_{q,0} == state0
-    put(rows - 2, S.I.has_thr0 ? (lam(7) - lam(6)) * isc : NAN);
-    put(rows - 1, S.I.has_steer0 ? (lam(9) - lam(8)) * isc : NAN);
+    put(rows - 2, S.I.has_thr0 ? yd(6) * isc : NAN);
+    put(rows - 1, S.I.has_steer0 ? yd(8) * isc : NAN);
   }
 }
 

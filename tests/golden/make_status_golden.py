@@ -1,0 +1,103 @@
+"""Generate tests/golden/status_ref_options.npz: the IPOPT status class at the reference's own options.
+
+TEST FIXTURE GENERATOR (build container only; the GPU box never runs the oracle's solves).
+
+The reference calls IPOPT with tol 1e-4, acceptable_tol 1e-2 (acceptable_iter: IPOPT's 15), max_iter 500
+(control/MPC.py:151-161, ControllerParameters.py:23).  SURVEY §8(c) lists the solver status class
+(converged / not converged) among the outputs that must match.  This script solves config 1 (the
+reference's script/test_mpc.py instance, dynamic and kinematic model) and the first 64 instances of C2, C4
+and C5 (mpcracing.workload.make_batch, deterministic) with oracle.ipopt.solve_ipopt under the FULL IPOPT
+rules (``ipopt.IPOPT``: soft restoration, tiny steps, the restoration phase's least-square multipliers,
+second-order corrections and watchdog included) in fp64 at exactly those options, and stores per instance
+the status (0 solved, 1 acceptable, 2 max_iter, 3 failed, 4 infeasible), the iteration count, why it
+stopped, the objective, the returned controls / states / progress and the unscaled constraint violation of
+the returned point.  tests/test_status_golden.py compares the product with it.
+
+Parity note: this pins the product against the RESTATEMENT of IPOPT's published rules; against IPOPT
+itself the status class stays unpinned (no IPOPT / CasADi in this image, none of its output in the
+reference).
+
+Usage: python tests/golden/make_status_golden.py [C1dyn C1kin C2 C4 C5]   (--procs 8)
+"""
+import json
+import os
+import sys
+import time
+from multiprocessing import Pool
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.abspath(os.path.join(HERE, "..", ".."))
+sys.path.insert(0, os.path.join(REPO, "mpc-racing_amd"))
+sys.path.insert(0, REPO)
+
+N_INST = 64
+OPTIONS = dict(tol=1e-4, acceptable_tol=1e-2, acceptable_iter=15, max_iter=500)
+OUT = os.path.join(HERE, "status_ref_options.npz")
+
+
+def _config(name):
+    from mpcracing import workload as wl
+    if name.startswith("C1"):
+        return dict(wl.CONFIGS["C1"], model=name[2:]), wl.make_batch("C1")
+    return wl.CONFIGS[name], wl.make_batch(name, limit=N_INST)
+
+
+def _n(name):
+    return 1 if name.startswith("C1") else N_INST
+
+
+def _solve(args):
+    import torch
+    torch.set_num_threads(1)
+    from mpcracing import workload as wl
+    from oracle.nlp import MPCProblem
+    from oracle.ipopt import IPOPT, solve_ipopt
+    name, i = args
+    cfg, b = _config(name)
+    tyres = wl.tyre_coeffs(cfg["tyres"]) if cfg["tyres"] else None
+    inst = wl.instance_dicts(b)[i]
+    p = MPCProblem(inst["state0"], inst["s0"], inst["cx"], inst["cy"], inst["max_error"], N=cfg["N"], Ts=cfg["Ts"],
+                   model=cfg["model"], lane_bounds=cfg["lane"], tyres=tyres)
+    t0 = time.time()
+    r = solve_ipopt(p, rules=IPOPT, **OPTIONS)
+    X, U, S, eC, eL = p.unpack(r.w)
+    w = torch.tensor(r.w, dtype=torch.float64)
+    d, dL, dU, _k = p.ipopt_ineq()
+    dv = d(w).numpy()
+    viol = max(float(np.abs(p.g(w).numpy()).max()),
+               float(np.maximum(0.0, np.maximum(np.where(np.isfinite(dL), dL - dv, 0.0),
+                                                np.where(np.isfinite(dU), dv - dU, 0.0))).max()))
+    return dict(i=i, status=r.status, iters=r.iters, obj=r.obj, kkt=r.kkt, viol=viol, why=r.why, X=X, U=U, S=S,
+                stats=r.stats, t=time.time() - t0)
+
+
+def main():
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    procs = int(next((a.split("=")[1] for a in sys.argv[1:] if a.startswith("--procs=")), 8))
+    names = args or ["C1dyn", "C1kin", "C2", "C4", "C5"]
+    jobs = [(n, i) for n in names for i in range(_n(n))]
+    with Pool(procs) as pool:
+        res = pool.map(_solve, jobs, chunksize=1)
+    out = dict(np.load(OUT)) if os.path.exists(OUT) else {}
+    for name in names:
+        rs = sorted([r for (n, _), r in zip(jobs, res) if n == name], key=lambda r: r["i"])
+        for k in ("X", "U", "S"):
+            out[f"{name}_{k}"] = np.stack([r[k] for r in rs], axis=-1)
+        for k in ("status", "iters"):
+            out[f"{name}_{k}"] = np.array([r[k] for r in rs], dtype=np.int32)
+        for k in ("obj", "kkt", "viol"):
+            out[f"{name}_{k}"] = np.array([r[k] for r in rs])
+        out[f"{name}_why"] = np.array([r["why"] for r in rs])
+        summ = {"config": name, "n": _n(name), "options": OPTIONS, "rules": "IPOPT",
+                "status_counts": np.bincount(out[f"{name}_status"], minlength=5).tolist(),
+                "status": out[f"{name}_status"].tolist(), "iters": out[f"{name}_iters"].tolist(),
+                "why": [r["why"] for r in rs], "seconds": round(sum(r["t"] for r in rs), 1),
+                "stats_total": {k: int(sum(r["stats"][k] for r in rs)) for k in rs[0]["stats"]}}
+        print(json.dumps(summ), flush=True)
+    np.savez_compressed(OUT, **out)
+
+
+if __name__ == "__main__":
+    main()
