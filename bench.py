@@ -497,6 +497,10 @@ def main():
                                    + (", lane-bound rows" if cfg["lane"] else ""),
                        "config_id": args.config, "N": cfg["N"], "instances_per_gpu": per,
                        "global_batch": int(tot[3]), "parallelism": f"dp{world} (instance shards)"},
+            # what the reference's opti.solve() accepts: IPOPT's "solved" and "solved to acceptable level"
+            # (status <= 1); the status-3 stops at the mu floor are the except branch
+            "solved_per_s": float(tot[4] + tot[5]) * args.steps / elapsed_max,
+            "solved_frac": float(tot[4] + tot[5]) / float(tot[3]),
             "p50_batch_latency_ms": float(np.median(kms)),
             "p50_latency_b1_ms": lat_b1_ms,
             "iters_mean": float(tot[1] / tot[3]),

@@ -742,8 +742,16 @@ struct SolveOut {
 #ifndef MR_F32_STALL
 #define MR_F32_STALL 15  // fp32 stall exit at the mu floor (iterations; 0 = off), see Solver::solve
 #endif
+// The line-search filter.  IPOPT's is unbounded; here it holds FCAP = FMAX + 64 FOVF entries, more than a
+// solve can add at max_iter <= 500 (at most one entry per iteration, the restoration phase's own filter
+// separate), so it never drops one there (the round-4 build kept the last 32, which the C3 audits showed
+// binding: 47-125 entries on long solves, profiles/r05_audit_C3_ipopt.json).  The wave kernel keeps the
+// first FMAX entries in LDS and the rest in the instance's cold fields (mr_wave.h CSF::FOV).
 #ifndef MR_FMAX
-#define MR_FMAX 32  // filter entries kept (IPOPT: unbounded; the oracle's longest filter on the audits is 32)
+#define MR_FMAX 32  // filter entries in LDS (wave kernel)
+#endif
+#ifndef MR_FOVF
+#define MR_FOVF 8   // overflow fields of 64 entries each (wave kernel: cold fields per bank)
 #endif
 #ifndef MR_FILTER_RESET_TRIGGER
 #define MR_FILTER_RESET_TRIGGER 5  // IPOPT filter_reset_trigger (0: heuristic off)
@@ -751,13 +759,20 @@ struct SolveOut {
 #ifndef MR_MAX_FILTER_RESETS
 #define MR_MAX_FILTER_RESETS 5  // IPOPT max_filter_resets
 #endif
-// IPOPT's tiny-step rule (tiny_step_tol 10 eps): off.  Its trigger is a step below 10 eps relative, i.e.
-// below the rounding noise of IPOPT's absolutely formed Lagrangian gradient at a converged point (the
-// oracle's dense restatement shows ~1e-14 relative steps there and never triggers it on the audited
-// instances); the correction-form residuals here are ~100x cleaner and would stop solves IPOPT continues.
+// IPOPT's tiny-step rule (tiny_step_tol 10 eps of double, tiny_step_y_tol 1e-2): a step below 10 eps
+// relative in every component of the reference's variables and slacks is taken without a line search and
+// forces a barrier decrease (at the smallest mu: "search direction becomes too small", status 3).  The
+// threshold is IPOPT's double epsilon in both precisions (an fp32 solve approximates IPOPT's fp64 one).
 #ifndef MR_TINY_STEP
 #define MR_TINY_STEP 0
 #endif
+// IPOPT's soft restoration phase (soft_resto_pderror_reduction_factor, max_soft_resto_iters)
+#ifndef MR_SOFT_RESTO
+#define MR_SOFT_RESTO 1
+#endif
+constexpr double IP_SOFT_RESTO_FACTOR = 0.9999;
+constexpr int IP_MAX_SOFT_RESTO = 10;
+constexpr double IP_TINY_STEP_TOL = 10.0 * 2.220446049250313e-16;
 #ifndef MR_LS_FAIL_MAX
 #define MR_LS_FAIL_MAX 1000000
 #endif
@@ -767,7 +782,7 @@ struct SolveOut {
 #ifndef MR_WD_TRIAL_MAX
 #define MR_WD_TRIAL_MAX 3  // IPOPT watchdog_trial_iter_max
 #endif
-constexpr int FMAX = MR_FMAX;
+constexpr int FMAX = MR_FMAX, FOVF = MR_FOVF, FCAP = MR_FMAX + 64 * MR_FOVF;
 
 // IPOPT 3.14 option defaults the solver restates beyond W&B 2006's line-search constants (the dense
 // restatement oracle/ipopt.py implements the same rules; DESIGN.md §2 lists them)
@@ -797,7 +812,7 @@ struct Solver {
   T mu, sc, delta_last;
   T alpha_p, alpha_d;  // last accepted primal / dual step (lazy update)
   T theta_max, theta_min;
-  T filt_th[FMAX], filt_ph[FMAX];
+  T filt_th[FCAP], filt_ph[FCAP];
   int nfilt;
   // iteration aggregates (eval sweep): dual infeasibility (stat), primal infeasibility of the equality
   // rows (pr_eq) and of the inequality rows' d - s (pr_rows; pr_max = both), the violation of the
@@ -811,10 +826,11 @@ struct Solver {
   bool resto = false;
   T rho = T(RESTO_RHO), zeta = T(0);
   T mu_o, th_entry, delta_last_o, theta_max_o, theta_min_o;
-  T ofilt_th[FMAX], ofilt_ph[FMAX];
+  T ofilt_th[FCAP], ofilt_ph[FCAP];
   int onfilt;
   T tho_acc, pho_acc;  // original theta / barrier objective of the last trial point (restoration)
   bool have_acc = false;  // an acceptable iterate is stored (AZ)
+  bool resto_first = false;  // the restoration phase's first iteration (no barrier update)
   double* trace = nullptr;  // optional per-iteration record (diagnostics)
   int trace_cap = 0;
   // the dynamics rows' multipliers nu_k (x_k = F(x_{k-1}, u_{k-1}), k >= 1) and their watchdog copy, fp64
@@ -1838,21 +1854,17 @@ struct Solver {
   }
 
   MR_HD bool filter_ok(T th, T ph) const {
-    for (int i = 0; i < FMAX; ++i)
-      if (i < nfilt && th >= filt_th[i] && ph >= filt_ph[i]) return false;
+    for (int i = 0; i < nfilt; ++i)
+      if (th >= filt_th[i] && ph >= filt_ph[i]) return false;
     return true;
   }
   MR_HD void filter_add(T th, T ph) {
     const T g_th = T(1e-5), g_ph = T(1e-5);
     const T a = (T(1) - g_th) * th, b = ph - g_ph * th;
-    if (nfilt < FMAX) {
+    if (nfilt < FCAP) {  // (full -- beyond max_iter 500 -- the entry is dropped, as in the wave kernel)
       filt_th[nfilt] = a;
       filt_ph[nfilt] = b;
       nfilt++;
-    } else {  // drop the oldest entry
-      for (int i = 0; i < FMAX - 1; ++i) { filt_th[i] = filt_th[i + 1]; filt_ph[i] = filt_ph[i + 1]; }
-      filt_th[FMAX - 1] = a;
-      filt_ph[FMAX - 1] = b;
     }
   }
 
@@ -2043,7 +2055,7 @@ struct Solver {
   MR_HD void resto_enter(T th, T ph) {
     filter_add(th, ph);
     onfilt = nfilt;
-    for (int i = 0; i < FMAX; ++i) { ofilt_th[i] = filt_th[i]; ofilt_ph[i] = filt_ph[i]; }
+    for (int i = 0; i < nfilt; ++i) { ofilt_th[i] = filt_th[i]; ofilt_ph[i] = filt_ph[i]; }
     mu_o = mu;
     th_entry = th;
     delta_last_o = delta_last;
@@ -2117,6 +2129,7 @@ struct Solver {
     alpha_p = alpha_d = T(0);
     mu = mu_r;
     resto = true;
+    resto_first = true;
     nfilt = 0;
     delta_last = T(0);
     theta_max = T(1e4) * mr_max(T(1), th_r);
@@ -2124,8 +2137,8 @@ struct Solver {
   }
   MR_HD bool resto_done() const {  // the accepted restoration step's point, seen by the original problem
     if (!(tho_acc <= T(RESTO_KAPPA) * th_entry)) return false;
-    for (int i = 0; i < FMAX; ++i)
-      if (i < onfilt && tho_acc >= ofilt_th[i] && pho_acc >= ofilt_ph[i]) return false;
+    for (int i = 0; i < onfilt; ++i)
+      if (tho_acc >= ofilt_th[i] && pho_acc >= ofilt_ph[i]) return false;
     return true;
   }
   MR_HD void resto_exit() {
@@ -2180,11 +2193,104 @@ struct Solver {
     alpha_p = alpha_d = T(0);
     mu = mu_o;
     nfilt = onfilt;
-    for (int i = 0; i < FMAX; ++i) { filt_th[i] = ofilt_th[i]; filt_ph[i] = ofilt_ph[i]; }
+    for (int i = 0; i < onfilt; ++i) { filt_th[i] = ofilt_th[i]; filt_ph[i] = ofilt_ph[i]; }
     theta_max = theta_max_o;
     theta_min = theta_min_o;
     delta_last = delta_last_o;
     resto = false;
+  }
+
+  // IPOPT's primal-dual system error (the soft restoration phase's measure; oracle/ipopt.py pd_error): the
+  // 1-norms of the Lagrangian gradient in the reference's variables (States, S_hat, U), of the slacks'
+  // stationarity -y - v_L + v_U, of the residuals c and d - s, and of v t - mu, at iterate buffer b with
+  // every multiplier stepped by a (0: the current ones).  Only ratios are used: the term count is not
+  // divided out.  (mr_wave.h pd_sweep: the same sums.)
+  MR_HD T pd_error(int b, T a) const {
+    T sum = T(0), sref_b = T(0), sref_u[2] = {T(0), T(0)}, sref_u0[2] = {T(0), T(0)}, sref_w[2] = {T(0), T(0)};
+    for (int k = 0; k <= N; ++k) {
+      T z[NZS], zn[NZS];
+      load_z(k, b, z);
+      T st[NZ], J[48];
+      double dd[NZ], nuk[NX], nun[NX];
+      for (int i = 0; i < NZ; ++i) { st[i] = T(0); dd[i] = 0.0; }
+      for (int i = 0; i < NX; ++i) nuk[i] = nub[k][i] + (double)a * (double)W(k, WF::DNU + i);
+      if (k < N) {
+        load_z(k + 1, b, zn);
+        for (int i = 0; i < NX; ++i) nun[i] = nub[k + 1][i] + (double)a * (double)W(k + 1, WF::DNU + i);
+        T Hd[36], fx[6], nz[NX];
+        for (int i = 0; i < NX; ++i) nz[i] = T(0);
+        Dyn<T, MODEL>::fjh(P, z, z + NX, nz, fx, J, Hd);
+        T xn[NX];
+        faug<T, MODEL>(P, k, z, xn);
+        for (int i = 0; i < NX; ++i) sum += mr_abs(xn[i] - zn[i]);
+        apply_At(J, k, nun, dd);
+        apply_Bt(J, k, nun, dd + NX);
+      }
+      for (int i = 0; i < NX; ++i) dd[i] -= nuk[i];
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      stage_cost(P, I, k, z, e, sc, st, (T*)nullptr);
+      T d[NI];
+      int act[NI];
+      Row<T> rows[NROW];
+      row_values(k, z, e, d, act, rows);
+      T lam_j[NI], y_j[NI];
+      for (int j = 0; j < NI; ++j) {
+        lam_j[j] = y_j[j] = T(0);
+        if (!act[j]) continue;
+        const T t = W(k, sf(b) + j);
+        lam_j[j] = W(k, WF::LAM + j) + a * W(k, WF::DLAM + j);
+        sum += mr_abs(lam_j[j] * t - mu);
+        if (yslot(j)) {
+          y_j[j] = W(k, WF::Y + j) + a * W(k, WF::DY + j);
+          sum += mr_abs(d[j] - t);
+        }
+      }
+      for (int r = 0; r <= NROW; ++r) {
+        const int j0 = r < NROW ? 2 * r : JL, j1 = j0 + 1;
+        if (!act[j0]) continue;
+        int idx[3];
+        T av[3];
+        const int na = row_grad(r, rows, e, idx, av);
+        T ys;
+        if (r < 2) {
+          ys = y_j[j0] + y_j[j1];
+          sum += mr_abs(-y_j[j0] - lam_j[j0]) + mr_abs(-y_j[j1] + lam_j[j1]);
+        } else {
+          ys = y_j[j0];
+          sum += mr_abs(-y_j[j0] - lam_j[j0] + lam_j[j1]);
+        }
+        for (int q = 0; q < na; ++q) st[idx[q]] += ys * av[q];
+      }
+      T sti[NZ];
+      for (int i = 0; i < NZ; ++i) sti[i] = T((double)st[i] + dd[i]);
+      for (int i = 0; i < 6; ++i) sum += mr_abs(sti[i]);  // X_k
+      const T bb = k < N ? sti[13] : T(0);
+      sum += mr_abs(sti[6] + sref_b - bb);  // S_k
+      sref_b = bb;
+      if (k >= 1)
+        for (int q = 0; q < 2; ++q) {
+          const T u = sref_u[q] + sti[7 + q];
+          if (k == 1) sref_u0[q] = u; else sum += mr_abs(u);
+          sref_w[q] += sti[9 + q];
+        }
+      if (k < N) { sref_u[0] = sti[11]; sref_u[1] = sti[12]; }
+      if (k == N)
+        for (int q = 0; q < 2; ++q) sum += mr_abs(sref_u0[q] + sref_w[q]);
+    }
+    return sum;
+  }
+  // IPOPT's TrySoftRestoStep (oracle/ipopt.py try_soft_resto): the full primal-dual step with one step size
+  // a = min(alpha_primal_max, alpha_dual_max); 1: accepted by the filter / sufficient-decrease test against
+  // the current point (an h-type step), 2: accepted by a primal-dual error reduction, 0: rejected.  The
+  // trial point is in buffer 1-cur; alpha = a.
+  MR_HD int soft_resto(const LSRef<T>& ref, T ap, T ad, T& alpha) {
+    const T a = mr_min(ap, ad);
+    alpha = a;
+    T th_t, ph_t;
+    if (!trial(a, false, th_t, ph_t)) return 0;
+    if (th_t <= theta_max && acc_to_iterate(th_t, ph_t, ref) && filter_ok(th_t, ph_t)) return 1;
+    return pd_error(1 - cur, a) <= T(IP_SOFT_RESTO_FACTOR) * pd_error(cur, T(0)) ? 2 : 0;
   }
 
   // IPOPT's tiny-step test (tiny_step_tol 10 eps): every component of the step of the reference's
@@ -2192,7 +2298,7 @@ struct Solver {
   // with primal infeasibility <= 1e-4.  ymall: also the multipliers' step below tiny_step_y_tol (1e-2).
   MR_HD bool tiny_step(bool& ysmall) const {
     if (!(pr_max <= T(1e-4))) return false;
-    const T tt = T(10) * mr_eps<T>();
+    const T tt = T(IP_TINY_STEP_TOL);
     ysmall = true;
     for (int k = 0; k <= N; ++k) {
       T z[NZS];
@@ -2233,7 +2339,8 @@ struct Solver {
     // successive iterations whose line search had a trial point rejected by the filter, clear it
     int filt_rej_iters = 0, filt_resets = 0;
     // watchdog state and the reference values of the point where it started
-    bool in_wd = false, tiny_flag = false;
+    bool in_wd = false, tiny_flag = false, in_soft = false;
+    int soft_count = 0;
     int wd_short = 0, wd_trial = 0;
     LSRef<T> wd_ref{T(0), T(0), T(0), T(0)};
     T wd_ap = T(0), wd_ad = T(0), wd_amin = T(0);
@@ -2283,7 +2390,9 @@ struct Solver {
       if (it >= P.max_iter) { out.status = 2; break; }
       T mu_old = mu;
       bool mu_stuck = false;
-      while (barrier_error(mu) <= kappa_eps * mu || tiny_flag) {
+      const bool skip_mu = resto && resto_first;  // IPOPT's MonotoneMuUpdate: none in the restoration phase's first iteration
+      resto_first = false;
+      while (!skip_mu && (barrier_error(mu) <= kappa_eps * mu || tiny_flag)) {
         const T m1 = kappa_mu * mu, m2 = mr_exp(theta_mu * mr_log(mu));
         const T mn = mr_max(mu_min, mr_min(m1, m2));
         if (mn == mu) { mu_stuck = tiny_flag; break; }
@@ -2292,10 +2401,12 @@ struct Solver {
       }
       if (mu_stuck) { out.status = 3; break; }  // tiny step at the smallest mu (IPOPT: search direction too small)
       tiny_flag = false;
-      if (mu != mu_old) {  // IPOPT resets its line search with a new barrier problem: filter and watchdog
+      if (mu != mu_old) {  // IPOPT resets its line search with a new barrier problem: filter, watchdog, soft resto
         nfilt = 0;
         in_wd = false;
         wd_short = 0;
+        in_soft = false;
+        soft_count = 0;
       }
       const T ph_cur = fval - mu * logs + T(IP_KAPPA_D) * mu * lins;  // the barrier objective (+ damping)
       // inertia-corrected factorisation (PDPerturbationHandler: delta = 0 first; then delta_xs_init 1e-4
@@ -2321,6 +2432,8 @@ struct Solver {
         mu_prev = mu;
         in_wd = false;
         wd_short = 0;
+        in_soft = false;
+        soft_count = 0;
         acc_count = 0;
         continue;
       }
@@ -2374,64 +2487,88 @@ struct Solver {
         acc_save();
         acc_kkt = out.kkt; acc_obj = out.obj; acc_viol = out.viol;
       }
-#if MR_WD_TRIGGER > 0
-      // IPOPT's watchdog (watchdog_shortened_iter_trigger, watchdog_trial_iter_max): after that many
-      // successive iterations whose accepted step was shorter than the fraction-to-boundary step, store
-      // the iterate and its search direction and take full steps tentatively; they are judged against
-      // the stored point (at its step size), and after watchdog_trial_iter_max iterations without an
-      // acceptable one the solver returns to the stored point and backtracks along its direction
-      // (skipping the full step)
-      if (!in_wd && wd_short >= MR_WD_TRIGGER) {
-        wd_save();
-        wd_ref = ref;
-        wd_ap = ap; wd_ad = ad; wd_amin = a_min;
-        in_wd = true;
-        wd_trial = 0;
-      }
-#endif
       T alpha = ap, a_test = ap, ph_acc = ph;
-      bool accepted = false, take_anyway = false, tiny = false, soc_taken = false;
+      bool accepted = false, take_anyway = false, tiny = false, soc_taken = false, soft_step = false,
+           soft_orig = false;
       int nls = 0;
       LSRef<T> used = ref;
-      bool ysmall = false;
-      if (MR_TINY_STEP && tiny_step(ysmall)) {  // IPOPT: a tiny step is taken without line search (and forces a mu decrease)
-        T th_t, ph_t;
-        trial(ap, false, th_t, ph_t);
-        accepted = tiny = true;
-        tiny_flag = ysmall;
-      } else if (in_wd) {
-        accepted = backtrack(ap, false, true, wd_ap, wd_ref, ap, alpha, a_test, ph_acc, nls, soc_taken);
-        used = wd_ref;
-        if (accepted) {
-          in_wd = false;
-          wd_short = 0;
-        } else if (++wd_trial <= MR_WD_TRIAL_MAX) {
-          take_anyway = true;  // the full step is taken tentatively
-          alpha = ap;
-          T th_t, ph_t;
-          trial(alpha, false, th_t, ph_t);
-        } else {
-          // back to the watchdog point: its iterate and direction, a regular backtracking line search
-          // that skips the full step
-          wd_restore();
-          in_wd = false;
-          wd_short = 0;
-          ref = wd_ref;
-          used = wd_ref;
-          ap = wd_ap; ad = wd_ad;
-          accepted = backtrack(ap, true, false, T(0), ref, wd_amin, alpha, a_test, ph_acc, nls, soc_taken);
-          th = ref.th; ph = ref.ph;
+      if (MR_SOFT_RESTO && in_soft) {
+        // the soft restoration phase continues (IPOPT: max_soft_resto_iters): its step replaces the line search
+        if (++soft_count <= IP_MAX_SOFT_RESTO) {
+          const int sr = soft_resto(ref, ap, ad, alpha);
+          if (sr) {
+            accepted = soft_step = true;
+            soft_orig = sr == 1;
+            if (soft_orig) { in_soft = false; soft_count = 0; }
+          }
         }
       } else {
-        accepted = backtrack(ap, false, false, T(0), ref, a_min, alpha, a_test, ph_acc, nls, soc_taken);
+#if MR_WD_TRIGGER > 0
+        // IPOPT's watchdog (watchdog_shortened_iter_trigger, watchdog_trial_iter_max): after that many
+        // successive iterations whose accepted step was shorter than the fraction-to-boundary step, store
+        // the iterate and its search direction and take full steps tentatively; they are judged against
+        // the stored point (at its step size), and after watchdog_trial_iter_max iterations without an
+        // acceptable one the solver returns to the stored point and backtracks along its direction
+        // (skipping the full step)
+        if (!in_wd && wd_short >= MR_WD_TRIGGER) {
+          wd_save();
+          wd_ref = ref;
+          wd_ap = ap; wd_ad = ad; wd_amin = a_min;
+          in_wd = true;
+          wd_trial = 0;
+        }
+#endif
+        bool ysmall = false;
+        if (MR_TINY_STEP && tiny_step(ysmall)) {  // IPOPT: a tiny step is taken without line search (and forces a mu decrease)
+          T th_t, ph_t;
+          trial(ap, false, th_t, ph_t);
+          accepted = tiny = true;
+          tiny_flag = ysmall;
+        } else if (in_wd) {
+          accepted = backtrack(ap, false, true, wd_ap, wd_ref, ap, alpha, a_test, ph_acc, nls, soc_taken);
+          used = wd_ref;
+          if (accepted) {
+            in_wd = false;
+            wd_short = 0;
+          } else if (++wd_trial <= MR_WD_TRIAL_MAX) {
+            take_anyway = true;  // the full step is taken tentatively
+            alpha = ap;
+            T th_t, ph_t;
+            trial(alpha, false, th_t, ph_t);
+          } else {
+            // back to the watchdog point: its iterate and direction, a regular backtracking line search
+            // that skips the full step
+            wd_restore();
+            in_wd = false;
+            wd_short = 0;
+            ref = wd_ref;
+            used = wd_ref;
+            ap = wd_ap; ad = wd_ad;
+            accepted = backtrack(ap, true, false, T(0), ref, wd_amin, alpha, a_test, ph_acc, nls, soc_taken);
+            th = ref.th; ph = ref.ph;
+          }
+        } else {
+          accepted = backtrack(ap, false, false, T(0), ref, a_min, alpha, a_test, ph_acc, nls, soc_taken);
+        }
+        if (MR_SOFT_RESTO && !accepted && !take_anyway) {
+          // IPOPT's soft restoration phase before the restoration phase proper (TrySoftRestoStep)
+          const int sr = soft_resto(ref, ap, ad, alpha);
+          if (sr) {
+            accepted = soft_step = true;
+            soft_orig = sr == 1;
+            in_soft = !soft_orig;
+            soft_count = 0;
+            used = ref;
+          }
+        }
       }
 #ifdef MR_RESTO_DEBUG
       if (trace) printf("   ls accepted %d take %d tiny %d alpha %.3e ap %.3e amin %.3e soc %d\n", (int)accepted, (int)take_anyway, (int)tiny, (double)alpha, (double)ap, (double)a_min, (int)soc_taken);
 #endif
       if (!accepted && !take_anyway) {
-        // IPOPT on a failed line search: (the soft restoration phase is not restated here)
-        // the current point acceptable -> "acceptable point reached"; almost feasible (theta <= 1e-2 tol)
-        // -> the stored acceptable point, or restoration failed; otherwise the restoration phase
+        // IPOPT on a failed line search (and failed soft restoration): the current point acceptable ->
+        // "acceptable point reached"; almost feasible (theta <= 1e-2 tol) -> the stored acceptable point, or
+        // restoration failed; otherwise the restoration phase
         if (acceptable(kkt)) { out.status = 1; break; }
         if (theta <= T(1e-2) * P.tol ||
             (sizeof(T) == 4 && mr_max(pr_eq, viol_max) <= T(IP_CONSTR_VIOL_TOL))) {  // fp32: feasible at its resolution
@@ -2448,6 +2585,8 @@ struct Solver {
         mu_prev = mu;
         in_wd = false;
         wd_short = 0;
+        in_soft = false;
+        soft_count = 0;
         acc_count = 0;
         if (trace && it < trace_cap) {
           double* tr = trace + 8 * it;
@@ -2457,7 +2596,7 @@ struct Solver {
         continue;
       }
       if (soc_taken) ad = wd_ad_of_commit();
-      if (!take_anyway && !tiny) wd_short = (alpha < ap) ? wd_short + 1 : 0;
+      if (!take_anyway && !tiny && !soft_step) wd_short = (alpha < ap) ? wd_short + 1 : 0;
 #if MR_FILTER_RESET_TRIGGER > 0
       if (filt_resets < MR_MAX_FILTER_RESETS) {
         filt_rej_iters = rej_filter ? filt_rej_iters + 1 : 0;
@@ -2468,9 +2607,11 @@ struct Solver {
         }
       }
 #endif
-      // IPOPT augments the filter unless the step is f-type with the Armijo condition
-      if (!take_anyway && !tiny && !(is_ftype(a_test, used) && armijo(ph_acc, a_test, used)))
+      // IPOPT augments the filter unless the step is f-type with the Armijo condition (a tiny step: never; a
+      // soft restoration step: only when the regular criterion accepted it -- an h-type step)
+      if (!take_anyway && (soft_step ? soft_orig : (!tiny && !(is_ftype(a_test, used) && armijo(ph_acc, a_test, used)))))
         filter_add(used.th, used.ph);
+      if (soft_step) ad = alpha;  // the soft restoration step moves every variable by one step size
       if (trace && it < trace_cap) {
         double* tr = trace + 8 * it;
         tr[0] = (double)kkt; tr[1] = (double)mu; tr[2] = (double)alpha; tr[3] = (double)ad;

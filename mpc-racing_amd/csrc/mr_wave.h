@@ -72,6 +72,9 @@
 #ifndef MR_RIC_AHEAD
 #define MR_RIC_AHEAD 2  // stages the Riccati's operand gathers run ahead of the factorisation (2 or 3)
 #endif
+#ifndef MR_MFMA_CHAIN
+#define MR_MFMA_CHAIN 1  // the forward / SOC recursions as MFMA products of the closed-loop map (0: lane-group dots)
+#endif
 #ifndef MR_PRIO_ITER
 #define MR_PRIO_ITER 0  // > 0: the wave raises its issue priority (s_setprio) at this iteration
 #endif
@@ -136,7 +139,10 @@ struct CSF {
     CP = RZ + NZS, CN = CP + 6, CVP = CN + 6, CVN = CVP + 6, CDP = CVN + 6, CDN = CDP + 6, CDVP = CDN + 6,
     CDVN = CDVP + 6, CSW = CDVN + 6, CGW0 = CSW + 6, CGW1 = CGW0 + 6,
     SJUNK = CGW1 + 6,  // discard slot of the SOC chains' lanes without a component
-    NF = SJUNK + 1
+    // the filter's entries beyond the FMAX in LDS (mr_solver.h FCAP): [bank][theta | phi][FOVF] fields, entry
+    // FMAX + 64 q + l in lane l of field q; bank 0 the original problem's, bank 1 the restoration phase's
+    FOV = SJUNK + 1,
+    NF = FOV + 4 * FOVF
   };
 };
 // The dynamics rows' multipliers nu (and their watchdog and acceptable-point snapshots) in fp64 whatever
@@ -151,7 +157,7 @@ MR_HD constexpr int64_t ws_words() { return WS_NU_OFF + 3 * NX * WL * (int64_t)(
 // solver objects, whose LDS footprint sets the occupancy.
 template <typename T>
 struct WaveCold {
-  int resto, in_wd, wd_short, wd_trial, onfilt, mrow, have_acc, tiny;
+  int resto, in_wd, wd_short, wd_trial, onfilt, mrow, have_acc, tiny, resto_first, in_soft, soft_count;
   T rho, zeta, mu_o, th_entry, delta_last_o, theta_max_o, theta_min_o, tho, pho;
   T wd_th, wd_ph, wd_gphi, wd_ap, wd_ad, wd_amin, wd_thpow;
   // evaluation aggregates beyond the solver object's (mr_solver.h Solver): primal infeasibility of the
@@ -288,7 +294,7 @@ struct WaveSolver {
 #else
   WaveShared<T> sh_store;
   T* filt = sh_store.filt;
-  MR_HD WaveCold<T>* cw() { return &sh_store.cold; }
+  MR_HD WaveCold<T>* cw() const { return const_cast<WaveCold<T>*>(&sh_store.cold); }
 #endif
   int nfilt;
   T stat_max, pr_max, theta, slam_max, slam_min, nu1, lam1, fval, logs;
@@ -460,6 +466,9 @@ struct WaveSolver {
     C->wd_trial = 0;
     C->have_acc = 0;
     C->tiny = 0;
+    C->resto_first = 0;
+    C->in_soft = 0;
+    C->soft_count = 0;
     C->delta_it = T(0);
   }
 
@@ -1436,6 +1445,187 @@ struct WaveSolver {
     }
   }
 
+  // ---------------- the closed-loop recursions on the matrix cores ----------------
+  // Given the factorisation (gains K_k, feed-forward kff_k), the forward substitution is the affine recursion
+  //   dx_{k+1} = Acl_k dx_k + w_k,   Acl = A + B K,  w = B kff + c   (dx_0 = 0),
+  // and a second-order correction's costate pass (soc_backward) is its transpose
+  //   pv_k = Acl_k^T pv_{k+1} + v_k.
+  // Each runs as one 16x16x4 MFMA product per stage on the augmented vector y = [x; 1] (rows 0..11):
+  //   y_{k+1} = M_k y_k,  M_k = [Acl_k | w_k ; 0 | 1]   (TR: y_k = M_k y_{k+1} with [Acl_k^T | v_k ; 0 | 1]),
+  // every column of the B operand a copy of y, three K-chunks (columns 0..11), the D result turned into
+  // the next B operand in registers (wtranspose4; fp64's D layout already is).  M_k's entries are formed
+  // per lane from the stage record -- entry (i, j) = base + p1 x1 + p2 x2, A + B K's structure: the vehicle
+  // rows' Jacobian J and the gains, the S / previous-control / frozen-copy rows' 0/1 entries from the
+  // record's constant slots (m_terms) -- gathered two stages ahead, so nothing beyond the Riccati's record
+  // is stored.  The critical path per stage is 3 MFMAs and 4 permutes instead of an 11-value broadcast
+  // and an 11-term dot (fwd_recursion's lane-group recursion, MR_MFMA_CHAIN=0).
+  // record offsets of entry (r, col) of M = [A + B K | B kff + c ; 0 | 1] (col 11: the affine column)
+  static MR_HD void m_terms(int r, int col, unsigned* t) {  // t = {base, p1, x1, p2, x2}
+    const unsigned Z = RCF::CZERO, O = RCF::CONE;
+    for (int q = 0; q < 5; ++q) t[q] = Z;
+    if (r >= 12 || col >= 12) return;
+    if (r == 11) { t[0] = col == 11 ? O : Z; return; }
+    const bool aff = col == 11;
+    auto kx = [&](int a) -> unsigned { return aff ? (unsigned)(RCF::K0 + a) : (unsigned)(RCF::K + a * NX + col); };
+    if (r < 6) {  // vehicle rows: J[r][col] (col < 6) + J[r][6] K[0][col] + J[r][7] K[1][col]
+      t[0] = aff ? RCF::C + r : (col < 6 ? RCF::J + r * 8 + col : Z);
+      t[1] = RCF::J + r * 8 + 6; t[2] = kx(0);
+      t[3] = RCF::J + r * 8 + 7; t[4] = kx(1);
+    } else if (r == 6) {  // S+ = S + dS
+      t[0] = aff ? RCF::C + 6 : (col == 6 ? O : Z); t[1] = O; t[2] = kx(2);
+    } else if (r == 7 || r == 8) {  // p+ = (thr, steer)
+      t[0] = aff ? RCF::C + r : Z; t[1] = O; t[2] = kx(r - 7);
+    } else {  // w+ = w (k > 0) or (thr, steer) (k = 0)
+      t[0] = aff ? RCF::C + r : (col == r ? RCF::SELP : Z); t[1] = RCF::SEL0; t[2] = kx(r - 9);
+    }
+  }
+  struct ChainRaw {
+    T t[3][5];  // the three fragments' gathered terms
+    T c[3];     // the affine column's cold replacements (SOCM: c_soc, k_soc; TR: v_k)
+  };
+  // TR: the transposed (costate) recursion, backward in k, v_k from the cold field SPV; SOCM: the affine
+  // column from the SOC's cold fields (c_soc in SC, k_soc in SK0).  Result rows y to LDX[row k] (TR) or
+  // [row k + 1] (forward); the caller provides row 0 (forward: dx_0 = 0) or row N (TR: pv_N) in y0.
+  template <bool TR, bool SOCM>
+  MR_HD void mfma_chain(const T* y0) {
+    const int N = wu(this->w, this->N), ln = this->ln;
+    const Wv w = this->w;
+    const WBuf<T> wb(rc - (int64_t)SSF::NF * WL, (unsigned)WS_NU_OFF);
+    auto R = [](int k) { return (unsigned)(SSF::NF * WL) + (unsigned)k * (unsigned)RC_STRIDE; };
+    const unsigned cold0 = (unsigned)(SSF::NF * WL) + (unsigned)RC_STRIDE * WL;
+    MR_LDS T* const LDX = lds + LDX_OFF;
+    const int i = ln & 15, g = ln >> 4;
+    unsigned off[3][5];
+    for (int s = 0; s < 3; ++s) {
+      const int j = 4 * s + g;
+      if (!TR) {
+        m_terms(i, j, off[s]);
+      } else {
+        for (int q = 0; q < 5; ++q) off[s][q] = RCF::CZERO;
+        if (i < 11 && j < 11) m_terms(j, i, off[s]);
+        else if (i == 11 && j == 11) off[s][0] = RCF::CONE;
+      }
+    }
+    // the affine column (lanes g = 3 of fragment 2, rows i < 11): its cold replacements
+    const bool aff = (SOCM || TR) && g == 3 && i < 11;
+    unsigned coff[3] = {(unsigned)CSF::SJUNK * WL, (unsigned)CSF::SJUNK * WL, (unsigned)CSF::SJUNK * WL};
+    if (aff) {
+      if (TR) {
+        coff[0] = (unsigned)(CSF::SPV + i) * WL;
+      } else {
+        const int a1 = i < 6 ? 0 : (i == 6 ? 2 : (i == 7 || i == 9 ? 0 : 1));
+        coff[0] = (unsigned)(CSF::SC + i) * WL;
+        coff[1] = (unsigned)(CSF::SK0 + a1) * WL;
+        coff[2] = (unsigned)(CSF::SK0 + 1) * WL;  // (x2 = kff[1] on the vehicle rows; p2 = 0 elsewhere)
+      }
+    }
+    auto cload = [&](int kk, ChainRaw& r) {
+      kk = kk < 0 ? 0 : (kk < N ? kk : N - 1);
+      const unsigned ro = (unsigned)wu(w, (int)R(kk));
+#pragma unroll
+      for (int s = 0; s < 3; ++s)
+#pragma unroll
+        for (int q = 0; q < 5; ++q) r.t[s][q] = wb.ld(ro, off[s][q]);
+      if constexpr (SOCM || TR) {
+        const unsigned co = (unsigned)wu(w, (int)(cold0 + (unsigned)kk));
+#pragma unroll
+        for (int q = 0; q < 3; ++q) r.c[q] = (TR && q > 0) ? T(0) : wb.ld(co, coff[q]);
+      }
+    };
+    // B operand: xb[s] = y[4s + g]
+    T xb[4] = {y0[0], y0[1], y0[2], T(0)};
+    // output rows: lane (g, c = 0) holds D rows drow(g, v)
+    const bool wr = (ln & 15) == 0;
+    auto cstep = [&](int k, const ChainRaw& r) {
+      T fr[3];
+#pragma unroll
+      for (int s = 0; s < 3; ++s) fr[s] = r.t[s][0] + r.t[s][1] * r.t[s][2] + r.t[s][3] * r.t[s][4];
+      if constexpr (TR) {
+        fr[2] = aff ? r.c[0] : fr[2];
+      } else if constexpr (SOCM) {
+        fr[2] = aff ? r.c[0] + r.t[2][1] * r.c[1] + r.t[2][3] * r.c[2] : fr[2];
+      }
+      T d[4] = {T(0), T(0), T(0), T(0)}, d2[4] = {T(0), T(0), T(0), T(0)};
+      wmfma(w, fr[0], xb[0], d);
+      wmfma(w, fr[2], xb[2], d2);
+      wmfma(w, fr[1], xb[1], d);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) d[v] += d2[v];
+      const int orow = TR ? k : k + 1;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int row = drow(g, v);
+        LDX[(wr && row < 12) ? orow * 12 + row : LJUNK_OFF - LDX_OFF + ln] = d[v];
+      }
+#pragma unroll
+      for (int v = 0; v < 4; ++v) xb[v] = d[v];
+      if constexpr (sizeof(T) == 4) wtranspose4(w, xb);
+    };
+    ChainRaw ra, rb2, rc2;
+    if constexpr (!TR) {
+      cload(0, ra);
+      cload(1, rb2);
+      for (int k = 0;; k += 3) {
+        if (k >= N) break;
+        cload(k + 2, rc2);
+        cstep(k, ra);
+        if (k + 1 >= N) break;
+        cload(k + 3, ra);
+        cstep(k + 1, rb2);
+        if (k + 2 >= N) break;
+        cload(k + 4, rb2);
+        cstep(k + 2, rc2);
+      }
+    } else {
+      cload(N - 1, ra);
+      cload(N - 2, rb2);
+      for (int k = N - 1;; k -= 3) {
+        if (k < 0) break;
+        cload(k - 2, rc2);
+        cstep(k, ra);
+        if (k - 1 < 0) break;
+        cload(k - 3, ra);
+        cstep(k - 1, rb2);
+        if (k - 2 < 0) break;
+        cload(k - 4, rb2);
+        cstep(k - 2, rc2);
+      }
+    }
+    wsync_lds(w);
+  }
+
+  // the forward substitution by mfma_chain, then stage-parallel: du_k = K_k dx_k + kff_k, the costate step
+  // dnu_k = P_k dx_k + p_k (SOCM: the SOC's kff and costate vector, into SDNU)
+  template <bool SOCM>
+  MR_HD void fwd_chain(T* dz) {
+    const int N = wu(this->w, this->N);
+    MR_LDS T* const LDX = lds + LDX_OFF;
+    const int g = ln >> 4;
+    T y0[3];
+    for (int s = 0; s < 3; ++s) y0[s] = (4 * s + g == 11) ? T(1) : T(0);
+    if (ln < 12) LDX[ln] = T(0);  // dx_0 = 0
+    mfma_chain<false, SOCM>(y0);
+    if (ln <= N) {
+      const int k = ln;
+      const MR_GLOBAL T* Rk = R(k);
+      T dx[NX];
+      for (int j = 0; j < NX; ++j) { dx[j] = LDX[k * 12 + j]; dz[j] = dx[j]; }
+      if (k < N)
+        for (int a = 0; a < NU; ++a) {
+          T v = SOCM ? Cf(CSF::SK0 + a) : Rk[RCF::K0 + a];
+          for (int j = 0; j < NX; ++j) v += Rk[RCF::K + a * NX + j] * dx[j];
+          dz[NX + a] = v;
+        }
+      for (int r = 0; r < NX; ++r) {
+        T v = SOCM ? Cf(CSF::SPV + r) : Rk[RCF::PV0 + r];
+        for (int j = 0; j < NX; ++j) v += Rk[RCF::P + pidx(r, j)] * dx[j];
+        if (k >= 1 || !MR_KKT_RESTATED) {  // k = 0: the initial-state rows' multiplier step
+          if constexpr (SOCM) Cf(CSF::SDNU + r) = v; else S(SSF::DNU + r) = v;
+        }
+      }
+    }
+  }
+
   // ---------------- sweep 3: forward substitution, slack/dual steps ----------------
   //   Sequential part: per stage, three lane groups share one 11-term dot with dx_k (gathered from
   //   lanes 0..10): [A | c] rows -> A dx_k + c, P_k rows -> the costate step, K_k rows -> du_k =
@@ -1451,7 +1641,11 @@ struct WaveSolver {
     const T tau = mr_max(T(0.99), T(1) - mu);
     T dz[NZS];
     for (int i = 0; i < NZS; ++i) dz[i] = T(0);
+#if MR_MFMA_CHAIN
+    fwd_chain<false>(dz);
+#else
     fwd_recursion<false>(dz);
+#endif
 #if MR_PHASE_CYCLES
     const unsigned long long tf1 = trace ? MR_CLOCK() : 0ull;
 #endif
@@ -1831,6 +2025,7 @@ struct WaveSolver {
       ntr++;
       flags |= fin ? LSR_FIN : 0;
       store = (mode & LS_FORCE) != 0;
+      if (store) ph_acc = ph_t;  // (the forced trial's own barrier objective: the soft restoration's test)
     } else {
       for (int n = 0; n < IP_LS_MAX; ++n) {
         if (!(alpha > a_min || n == 0)) break;
@@ -1980,6 +2175,68 @@ struct WaveSolver {
       for (int i = 0; i < NZ; ++i) Cf(CSF::SG + i) = g[i];
     }
     wsync(w);
+#if MR_MFMA_CHAIN
+    // pv_k = Acl_k^T pv_{k+1} + v_k with v_k = A_k^T q + K_k^T u_k + g_x, q = P_{k+1} c_k, u_k = B_k^T q + g_u
+    // (then r_k = B_k^T pv_{k+1} + u_k): v_k, u_k stage-parallel into the cold fields SPV / SK0, the
+    // recursion by mfma_chain<TR>, then r_k and the feed-forward stage-parallel
+    if (own() && ln < N) {
+      const int k = ln;
+      const MR_GLOBAL T* Rk = R(k);
+      const MR_GLOBAL T* Rn = R(k + 1);
+      T c[NX], q[NX], J[48];
+      for (int j = 0; j < NX; ++j) c[j] = Cf(CSF::SC + j);
+      for (int r = 0; r < NX; ++r) {
+        T v = T(0);
+        for (int j = 0; j < NX; ++j) v += Rn[RCF::P + pidx(r, j)] * c[j];
+        q[r] = v;
+      }
+      for (int j = 0; j < 48; ++j) J[j] = Rk[RCF::J + j];
+      T u[NU], at[NX];
+      apply_Bt(J, k, q, u);
+      for (int a = 0; a < NU; ++a) u[a] += Cf(CSF::SG + NX + a);
+      apply_At(J, k, q, at);
+      for (int r = 0; r < NX; ++r) {
+        T v = at[r] + Cf(CSF::SG + r);
+        for (int a = 0; a < NU; ++a) v += Rk[RCF::K + a * NX + r] * u[a];
+        Cf(CSF::SPV + r) = v;
+      }
+      for (int a = 0; a < NU; ++a) Cf(CSF::SK0 + a) = u[a];
+    }
+    MR_LDS T* const LDX = lds + LDX_OFF;
+    {  // pv_N = g_x,N: the chain's start (B operand rows 4s + g) and LDX row N
+      const int g = ln >> 4;
+      const MR_GLOBAL T* cbN = rc + (int64_t)RC_STRIDE * WL + N;
+      T y0[3];
+      for (int s2 = 0; s2 < 3; ++s2) {
+        const int r = 4 * s2 + g;
+        y0[s2] = r < NX ? cbN[(CSF::SG + (r < NX ? r : 0)) * WL] : (r == 11 ? T(1) : T(0));
+      }
+      if (ln < NX) LDX[N * 12 + ln] = cbN[(CSF::SG + ln) * WL];
+      wsync(w);  // v_k, u_k (cold fields) and row N visible
+      mfma_chain<true, false>(y0);
+    }
+    if (own()) {
+      const int k = ln;
+      T pv[NX];
+      for (int r = 0; r < NX; ++r) pv[r] = LDX[k * 12 + r];
+      if (k < N) {
+        const MR_GLOBAL T* Rk = R(k);
+        T J[48], pn[NX], r3[NU];
+        for (int j = 0; j < 48; ++j) J[j] = Rk[RCF::J + j];
+        for (int r = 0; r < NX; ++r) pn[r] = LDX[(k + 1) * 12 + r];
+        apply_Bt(J, k, pn, r3);
+        const T Lf[6] = {T(0), Rk[RCF::LQ + 0], T(0), Rk[RCF::LQ + 1], Rk[RCF::LQ + 2], T(0)};
+        const T iv[3] = {Rk[RCF::LQ + 3], Rk[RCF::LQ + 4], Rk[RCF::LQ + 5]};
+        T kf[NU];
+        for (int a = 0; a < NU; ++a) kf[a] = -(r3[a] + Cf(CSF::SK0 + a));
+        lsolve3r(Lf, iv, kf);
+        ltsolve3r(Lf, iv, kf);
+        for (int a = 0; a < NU; ++a) Cf(CSF::SK0 + a) = kf[a];
+      }
+      for (int r = 0; r < NX; ++r) Cf(CSF::SPV + r) = pv[r];
+    }
+    wsync(w);
+#else
     const MR_GLOBAL T* cb = rc + (int64_t)RC_STRIDE * WL;
     const WBuf<T> wb(rc + (int64_t)RC_STRIDE * WL, (unsigned)CSF::NF * WL);
     const bool row = ln < NX;
@@ -2068,6 +2325,7 @@ struct WaveSolver {
       for (int a = 0; a < NU; ++a) Cf(CSF::SK0 + a) = kf[a];
     }
     wsync(w);
+#endif
   }
   // the SOC direction (mr_solver.h Solver::forward with soc set): SDZ, SDS, SDLAM, SDY, SDNU.  The recursion
   // is the Newton direction's (fwd_recursion, its lane groups and prefetch) with the SOC's feed-forward,
@@ -2082,7 +2340,11 @@ struct WaveSolver {
 #if MR_PHASE_CYCLES
     const unsigned long long tc0 = trace ? MR_CLOCK() : 0ull;
 #endif
+#if MR_MFMA_CHAIN
+    fwd_chain<true>(dzr);
+#else
     fwd_recursion<true>(dzr);
+#endif
     wsync(w);  // SDNU (the recursion's costate steps) visible
 #if MR_PHASE_CYCLES
     if (trace) tsub[2] += MR_CLOCK() - tc0;
@@ -2147,9 +2409,24 @@ struct WaveSolver {
     return ad;
   }
 
+  // The filter: entries 0..FMAX-1 in LDS (every lane the same values), the rest in the cold fields FOV of
+  // the phase's bank, lane l holding entries FMAX + 64 q + l (one coalesced load per 64 entries, tested
+  // stage-parallel and OR-reduced) -- IPOPT's unbounded filter up to FCAP entries (mr_solver.h)
+  MR_HD int fbank() const { return cw()->resto ? 1 : 0; }
+  MR_HD bool filter_hit_ov(T th, T ph, int n, int bank) const {
+    int hit = 0;
+    for (int q = 0; q < FOVF; ++q) {
+      const int base = FMAX + q * WL;
+      if (base >= n) break;  // (n wave-uniform)
+      const T a = Cf(CSF::FOV + (2 * bank) * FOVF + q), b = Cf(CSF::FOV + (2 * bank + 1) * FOVF + q);
+      hit |= (base + ln < n && th >= a && ph >= b) ? 1 : 0;
+    }
+    return wmax(w, hit) != 0;
+  }
   MR_HD bool filter_ok(T th, T ph) const {
     for (int i = 0; i < FMAX; ++i)
       if (i < nfilt && th >= fth(i) && ph >= fph(i)) return false;
+    if (nfilt > FMAX && filter_hit_ov(th, ph, nfilt, fbank())) return false;
     return true;
   }
   MR_HD void filter_add(T th, T ph) {
@@ -2157,10 +2434,14 @@ struct WaveSolver {
       for (int i = 0; i < FMAX; ++i)
         if (i == nfilt) { fth(i) = th; fph(i) = ph; }
       nfilt++;
-    } else {
-      for (int i = 0; i < FMAX - 1; ++i) { fth(i) = fth(i + 1); fph(i) = fph(i + 1); }
-      fth(FMAX - 1) = th;
-      fph(FMAX - 1) = ph;
+    } else if (nfilt < FCAP) {  // (full -- beyond max_iter 500 -- the entry is dropped, as in mr_solver.h)
+      const int o = nfilt - FMAX, b = fbank();
+      if (ln == (o & (WL - 1))) {
+        Cf(CSF::FOV + (2 * b) * FOVF + (o >> 6)) = th;
+        Cf(CSF::FOV + (2 * b + 1) * FOVF + (o >> 6)) = ph;
+      }
+      nfilt++;
+      wsync(w);  // the entry visible to every lane's later filter tests
     }
   }
 
@@ -2277,6 +2558,9 @@ struct WaveSolver {
     alpha_p = alpha_d = T(0);
     mu = mu_r;
     C->resto = 1;
+    C->resto_first = 1;  // no barrier update in the restoration phase's first iteration
+    C->in_soft = 0;
+    C->soft_count = 0;
     nfilt = 0;
     delta_last = T(0);
     theta_max = T(1e4) * mr_max(T(1), th_r);
@@ -2289,6 +2573,7 @@ struct WaveSolver {
     bool ok = tho <= T(RESTO_KAPPA) * C->th_entry;
     for (int i = 0; i < FMAX; ++i)
       if (i < C->onfilt && tho >= C->ofilt[i] && pho >= C->ofilt[FMAX + i]) ok = false;
+    if (C->onfilt > FMAX && filter_hit_ov(tho, pho, C->onfilt, 0)) ok = false;  // the original filter's bank
     return wuni(w, ok);
   }
   MR_SWEEP void resto_exit() {
@@ -2386,6 +2671,177 @@ struct WaveSolver {
     wsync(w);
   }
 
+  // IPOPT's primal-dual system error (the soft restoration phase's measure; oracle/ipopt.py pd_error): the
+  // 1-norms of the Lagrangian gradient in the reference's variables (States, S_hat, U), of the slacks'
+  // stationarity -y - v_L + v_U, of the equality residuals c and d - s, and of v t - mu, at the current
+  // iterate (TRIAL false) or at the trial point in buffer 1-cur with every multiplier stepped by a (the soft
+  // restoration step's one step size).  Only its ratio between two points is used, so the count of terms
+  // (equal at both) is not divided out.  Stage-parallel, like eval_sweep's stationarity (fp64 dynamics
+  // multipliers, correction-form dd); rare (failed line searches only), so the Hessian the generated
+  // dynamics code computes alongside is simply discarded.  Result in res_th.
+  template <bool TRIAL>
+  MR_SWEEP void pd_sweep(T a) {
+    MR_UNIFORM_P();
+    MR_ASSUME_LDS_STATE();
+    const int k = ln, b = TRIAL ? 1 - cur : cur;
+    const double ad = TRIAL ? (double)a : 0.0;
+    const T at = TRIAL ? a : T(0);
+    T z[NZS];
+    load_z(b, z);
+    T znext[NX];
+    for (int i = 0; i < NX; ++i) znext[i] = wnext(w, z[i]);
+    double nuk[NX];
+    for (int i = 0; i < NX; ++i) nuk[i] = (own() && (k >= 1 || !MR_KKT_RESTATED)) ? NUd(i) + ad * (double)S(SSF::DNU + i) : 0.0;
+    double nnd[NX];
+    for (int i = 0; i < NX; ++i) nnd[i] = wnext(w, own() && k >= 1 ? nuk[i] : 0.0);
+    T sum_l = T(0), rs_a = T(0), rs_b = T(0), rs_u[2] = {T(0), T(0)}, rs_p[2] = {T(0), T(0)}, rs_w[2] = {T(0), T(0)};
+    if (own()) {
+      T st[NZ], J[48];
+      double dd[NZ];
+      for (int i = 0; i < NZ; ++i) { st[i] = T(0); dd[i] = 0.0; }
+      for (int i = 0; i < 48; ++i) J[i] = T(0);
+      if (k < N) {
+        T Hd[36], fx[6], nz[NX];
+        for (int i = 0; i < NX; ++i) nz[i] = T(0);
+        Dyn<T, MODEL>::fjh(P, z, z + NX, nz, fx, J, Hd);
+        T c[NX];
+        for (int i = 0; i < 6; ++i) c[i] = fx[i] - znext[i];
+        c[6] = z[6] + z[13] - znext[6];
+        c[7] = z[11] - znext[7];
+        c[8] = z[12] - znext[8];
+        c[9] = (k == 0 ? z[11] : z[9]) - znext[9];
+        c[10] = (k == 0 ? z[12] : z[10]) - znext[10];
+        for (int i = 0; i < NX; ++i) sum_l += mr_abs(c[i]);
+        apply_At(J, k, nnd, dd);
+        apply_Bt(J, k, nnd, dd + NX);
+      }
+      for (int i = 0; i < NX; ++i) dd[i] -= nuk[i];
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      stage_cost(P, I, k, z, e, sc, st, (T*)nullptr);
+      T d[NI];
+      int act[NI];
+      row_values(k, z, e, d, act);
+      T lam_j[NI], t_j[NI], y_j[NI];
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        lam_j[j] = y_j[j] = T(0);
+        t_j[j] = T(1);
+        if (!act[j]) continue;
+        const T t = S(sf(b) + j), lam = S(SSF::LAM + j) + at * S(SSF::DLAM + j);
+        lam_j[j] = lam;
+        t_j[j] = t;
+        sum_l += mr_abs(lam * t - mu);
+        if (yslot(j)) {
+          y_j[j] = S(SSF::Y + j) + at * S(SSF::DY + j);
+          sum_l += mr_abs(d[j] - t);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < NROW; ++r) {
+        const int j0 = 2 * r, j1 = j0 + 1;
+        if (!act[j0]) continue;
+        T ys;
+        if (r < 2) {
+          ys = y_j[j0] + y_j[j1];
+          sum_l += mr_abs(-y_j[j0] - lam_j[j0]) + mr_abs(-y_j[j1] + lam_j[j1]);
+        } else {
+          ys = y_j[j0];
+          sum_l += mr_abs(-y_j[j0] - lam_j[j0] + lam_j[j1]);
+        }
+#pragma unroll
+        for (int q = 0; q < RN(r); ++q) st[RI(r, q)] += ys * T(RS(q));
+      }
+      if (lane_active(P, k)) {
+        const T ys = y_j[JL];
+        sum_l += mr_abs(-ys - lam_j[JL] + lam_j[JL + 1]);
+        st[0] += ys * e.gC[0];
+        st[1] += ys * e.gC[1];
+        st[6] += ys * e.gC[2];
+      }
+      T sti[NZ];
+      for (int i = 0; i < NZ; ++i) sti[i] = T((double)st[i] + dd[i]);
+      for (int i = 0; i < 6; ++i) sum_l += mr_abs(sti[i]);  // X_k (k = 0: with the initial-state rows' nu_0)
+      rs_a = sti[6];
+      rs_b = k < N ? sti[13] : T(0);
+      if (k < N) { rs_u[0] = sti[11]; rs_u[1] = sti[12]; }
+      if (k >= 1) { rs_p[0] = sti[7]; rs_p[1] = sti[8]; rs_w[0] = sti[9]; rs_w[1] = sti[10]; }
+    }
+    // S_k = S_k + Delta-S_{k-1} - Delta-S_k; U_k = u_k + p_{k+1} (U_0: + every w_j), as eval_sweep
+    const T bprev = wprev(w, rs_b), pn0 = wnext(w, rs_p[0]), pn1 = wnext(w, rs_p[1]);
+    const T ws0 = wsum(w, rs_w[0]), ws1 = wsum(w, rs_w[1]);
+    if (own()) {
+      sum_l += mr_abs(rs_a + (k >= 1 ? bprev : T(0)) - rs_b);
+      if (k < N) {
+        sum_l += mr_abs(rs_u[0] + pn0 + (k == 0 ? ws0 : T(0)));
+        sum_l += mr_abs(rs_u[1] + pn1 + (k == 0 ? ws1 : T(0)));
+      }
+    }
+    res_th = wsum(w, sum_l);
+  }
+
+  // IPOPT's TrySoftRestoStep (oracle/ipopt.py try_soft_resto): the full primal-dual step with one step size
+  // a = min(alpha_primal_max, alpha_dual_max); accepted if the filter / sufficient-decrease test against the
+  // current point passes (1: "accepted by the original criterion", an h-type step), else if the primal-dual
+  // error falls by soft_resto_pderror_reduction_factor (2); 0 rejected.  The trial point is in buffer 1-cur,
+  // res_alpha = a.
+  MR_HD int soft_resto(T th, T ph, T gphi, T th_pow, T ap, T ad) {
+    const T a = mr_min(ap, ad);
+    line_search<false, false>(th, ph, gphi, th_pow, a, a, a, 0, LS_FORCE, a, T(-1));
+    if (!(res_flags & LSR_FIN)) return 0;
+    const T th_t = res_th, ph_t = res_ph;
+    const LSRef<T> ref{th, ph, gphi, th_pow};
+    int r = 0;
+    if (th_t <= theta_max && acc_to_iterate(th_t, ph_t, ref) && filter_ok(th_t, ph_t)) {
+      r = 1;
+    } else {
+      pd_sweep<true>(a);
+      const T pd_t = res_th;
+      pd_sweep<false>(T(0));
+      r = pd_t <= T(IP_SOFT_RESTO_FACTOR) * res_th ? 2 : 0;
+    }
+    res_alpha = a;
+    return r;
+  }
+
+  // IPOPT's tiny-step test (mr_solver.h Solver::tiny_step; tiny_step_tol 10 eps of double, IPOPT's): at a point
+  // with primal infeasibility <= 1e-4, every step component of the reference's variables (global X, Y, S)
+  // and of IPOPT's slacks below 10 eps relative to 1 + |value|.  res_flags: 1 tiny, 2 the multipliers' steps
+  // also below tiny_step_y_tol (1e-2).  Lane = stage, AND-reduced.
+  MR_SWEEP void tiny_check() {
+    MR_UNIFORM_P();
+    MR_ASSUME_LDS_STATE();
+    int tiny_l = 1, ys_l = 1;
+    if (own()) {
+      const int k = ln;
+      const T tt = T(IP_TINY_STEP_TOL);
+      T z[NZS];
+      load_z(cur, z);
+      for (int i = 0; i < NZ; ++i) {
+        if (!delta_var(i) || (k == 0 && i <= 6) || (k == N && i >= NX)) continue;
+        const T org = i == 0 ? I.org[0] : (i == 1 ? I.org[1] : (i == 6 ? I.org[2] : T(0)));
+        if (mr_abs(S(SSF::DZ + i)) > tt * (T(1) + mr_abs(z[i] + org))) tiny_l = 0;
+      }
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      T d[NI];
+      int act[NI];
+      row_values(k, z, e, d, act);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        if (!act[j] || !yslot(j)) continue;
+        const T c = j < JL ? row_c(j / 2, z) : e.eC;
+        const T sv = c - T(slot_sign(j)) * (d[j] - S(sf(cur) + j));  // IPOPT's slack value
+        if (mr_abs(S(SSF::DS + j)) > tt * (T(1) + mr_abs(sv))) tiny_l = 0;
+        if (!(mr_abs(S(SSF::DY + j)) < T(1e-2))) ys_l = 0;
+      }
+      for (int i = 0; i < NX; ++i)
+        if ((i < 6 || (k == 0 && i == 6)) && !(mr_abs(S(SSF::DNU + i)) < T(1e-2))) ys_l = 0;
+    }
+    const int t = wmin(w, tiny_l), y = wmin(w, ys_l);
+    res_flags = (t ? 1 : 0) | (y ? 2 : 0);
+  }
+
   // ---------------- the IPM loop (wave-uniform control; mr_solver.h Solver::solve, same rules) ----------------
   MR_HD SolveOut solve() {
     MR_UNIFORM_P();
@@ -2466,17 +2922,27 @@ struct WaveSolver {
         }
       }
       if (it >= P.max_iter) { out.status = 2; break; }
+      // IPOPT's monotone barrier update; a tiny step forces a decrease (at the smallest mu: "search direction
+      // becomes too small", status 3); none in the restoration phase's first iteration (MonotoneMuUpdate)
       T mu_old = mu;
-      while (barrier_error(mu) <= kappa_eps * mu) {
+      bool tflag = cw()->tiny != 0, mu_stuck = false;
+      const bool skip_mu = rs && cw()->resto_first != 0;
+      cw()->tiny = 0;
+      cw()->resto_first = 0;
+      while (!skip_mu && (barrier_error(mu) <= kappa_eps * mu || tflag)) {
         const T m1 = kappa_mu * mu, m2 = mr_exp(theta_mu * mr_log(mu));
         const T mn = mr_max(mu_min, mr_min(m1, m2));
-        if (mn == mu) break;
+        if (mn == mu) { mu_stuck = tflag; break; }
         mu = mn;
+        tflag = false;
       }
-      if (mu != mu_old) {  // IPOPT resets its line search with a new barrier problem: filter and watchdog
+      if (mu_stuck) { out.status = 3; break; }
+      if (mu != mu_old) {  // IPOPT resets its line search with a new barrier problem: filter, watchdog, soft restoration
         nfilt = 0;
         cw()->in_wd = 0;
         cw()->wd_short = 0;
+        cw()->in_soft = 0;
+        cw()->soft_count = 0;
       }
       const T ph_cur = fval - mu * logs + T(IP_KAPPA_D) * mu * cw()->lins;  // barrier objective (+ damping)
       // inertia-corrected factorisation (IPOPT's PDPerturbationHandler, mr_solver.h)
@@ -2558,101 +3024,139 @@ struct WaveSolver {
         acc_save();
         acc_kkt = out.kkt; acc_obj = out.obj; acc_viol = out.viol;
       }
-#if MR_WD_TRIGGER > 0
-      // IPOPT's watchdog (mr_solver.h, same rule): after watchdog_shortened_iter_trigger successive
-      // shortened steps store the iterate and direction, take full steps tentatively, judged against the
-      // stored point at its step size; after watchdog_trial_iter_max without an acceptable one, back to the
-      // stored point and a regular backtracking line search that skips the full step
-      if (!cw()->in_wd && cw()->wd_short >= MR_WD_TRIGGER) {
-        wd_save();
-        auto* C = cw();
-        C->wd_th = th; C->wd_ph = ph; C->wd_gphi = gphi; C->wd_ap = ap; C->wd_ad = ad; C->wd_amin = a_min;
-        C->wd_thpow = th_pow;
-        C->in_wd = 1;
-        C->wd_trial = 0;
-      }
-#endif
-      bool take_anyway = false, accepted = false, soc_taken = false, rejf = false;
+      bool take_anyway = false, accepted = false, soc_taken = false, rejf = false, tiny = false, soft_step = false,
+           soft_orig = false;
       T alpha = ap;
       T uth = th, uph = ph;  // the accepting line search's reference (the filter entry on augmentation)
       int flags = 0;
       MR_T0();
-      if (wuni(w, cw()->in_wd != 0)) {
-        auto* C = cw();
-        line_search<false, false>(C->wd_th, C->wd_ph, C->wd_gphi, C->wd_thpow, ap, ap, ap, 0, LS_WD, C->wd_ap,
-                                  T(-1));
-        flags = res_flags;
-        rejf |= (flags & LSR_REJF) != 0;
-        uth = C->wd_th;
-        uph = C->wd_ph;
-        if (flags & LSR_ACC) {
-          accepted = true;
-          C->in_wd = 0;
-          C->wd_short = 0;
-        } else if (++C->wd_trial <= MR_WD_TRIAL_MAX) {
-          take_anyway = true;  // the full step is taken tentatively (LS_WD stored that trial point already)
-        } else {
-          // back to the watchdog point: its iterate and direction, a regular backtracking line search
-          // that skips the full step
-          wd_restore();
-          C->in_wd = 0;
-          C->wd_short = 0;
-          th = C->wd_th; ph = C->wd_ph; gphi = C->wd_gphi; ap = C->wd_ap; ad = C->wd_ad; a_min = C->wd_amin;
-          th_pow = C->wd_thpow;
-          line_search<false, false>(th, ph, gphi, th_pow, T(0.5) * ap, ap, a_min, 1, LS_NOSOC, T(0), T(-1));
-          flags = res_flags;
-          rejf |= (flags & LSR_REJF) != 0;
-          accepted = (flags & LSR_ACC) != 0;
+      if (MR_SOFT_RESTO && wuni(w, cw()->in_soft != 0)) {
+        // the soft restoration phase continues (IPOPT: max_soft_resto_iters): its step replaces the line search
+        if (++cw()->soft_count <= IP_MAX_SOFT_RESTO) {
+          const int sr = soft_resto(th, ph, gphi, th_pow, ap, ad);
+          if (sr) {
+            accepted = soft_step = true;
+            soft_orig = sr == 1;
+            if (soft_orig) { cw()->in_soft = 0; cw()->soft_count = 0; }
+          }
         }
       } else {
-        line_search<false, false>(th, ph, gphi, th_pow, ap, ap, a_min, 0, 0, T(0), T(-1));
-        flags = res_flags;
-        rejf |= (flags & LSR_REJF) != 0;
-        accepted = (flags & LSR_ACC) != 0;
-        if (flags & LSR_NEED_SOC) {
-          // IPOPT's TrySecondOrderCorrection: up to max_soc (4) linear corrections while theta falls by
-          // kappa_soc (0.99); then, if none is accepted, the backtracking resumes at alpha / 2
-          const T a_trial = res_alpha, a_test0 = res_atest;
-          T th_trial = res_th, a_soc = a_trial, th_old = T(0);
-          soc_prepare();
-          for (int count = 0; count < IP_MAX_SOC; ++count) {
-            if (count > 0 && !(th_trial <= T(IP_KAPPA_SOC) * th_old)) break;
-            th_old = th_trial;
-            if (count == 0)
-              line_search<false, false>(th, ph, gphi, th_pow, a_soc, ap, a_min, 0, LS_ACC, a_soc, a_soc);
-            else
-              line_search<false, true>(th, ph, gphi, th_pow, a_soc, ap, a_min, 0, LS_ACC, a_soc, a_soc);
-            MR_STAT(st_soc_try++);
-            MR_CNT(5);
-#if MR_PHASE_CYCLES
-            const unsigned long long ts0 = trace ? MR_CLOCK() : 0ull;
+#if MR_WD_TRIGGER > 0
+        // IPOPT's watchdog (mr_solver.h, same rule): after watchdog_shortened_iter_trigger successive
+        // shortened steps store the iterate and direction, take full steps tentatively, judged against the
+        // stored point at its step size; after watchdog_trial_iter_max without an acceptable one, back to the
+        // stored point and a regular backtracking line search that skips the full step
+        if (!cw()->in_wd && cw()->wd_short >= MR_WD_TRIGGER) {
+          wd_save();
+          auto* C = cw();
+          C->wd_th = th; C->wd_ph = ph; C->wd_gphi = gphi; C->wd_ap = ap; C->wd_ad = ad; C->wd_amin = a_min;
+          C->wd_thpow = th_pow;
+          C->in_wd = 1;
+          C->wd_trial = 0;
+        }
 #endif
-            soc_backward();
-#if MR_PHASE_CYCLES
-            const unsigned long long ts1 = trace ? MR_CLOCK() : 0ull;
-#endif
-            T aps, ads;
-            forward_soc(aps, ads);
-#if MR_PHASE_CYCLES
-            if (trace) { tsub[6] += ts1 - ts0; tsub[7] += MR_CLOCK() - ts1; }
-#endif
-            line_search<false, true>(th, ph, gphi, th_pow, aps, aps, aps, 0, LS_WD, a_test0, T(-1));
-            rejf |= (res_flags & LSR_REJF) != 0;
-            a_soc = aps;
-            if (!(res_flags & LSR_FIN)) break;
-            if (res_flags & LSR_ACC) {
-              soc_taken = accepted = true;
-              flags = res_flags;
-              ad = soc_commit();
-              break;
-            }
-            th_trial = res_th;
-          }
-          if (!soc_taken) {
-            line_search<false, false>(th, ph, gphi, th_pow, T(0.5) * a_trial, ap, a_min, 1, LS_NOSOC, T(0), T(-1));
+        bool ysmall = false;
+        if (MR_TINY_STEP) {
+          tiny_check();
+          tiny = (res_flags & 1) != 0;
+          ysmall = (res_flags & 2) != 0;
+        }
+        if (tiny) {  // IPOPT: a tiny step is taken without a line search (and, with small multiplier steps,
+                     // forces a barrier decrease)
+          line_search<false, false>(th, ph, gphi, th_pow, ap, ap, ap, 0, LS_FORCE, ap, T(-1));
+          accepted = true;
+          cw()->tiny = ysmall ? 1 : 0;
+        } else if (wuni(w, cw()->in_wd != 0)) {
+          auto* C = cw();
+          line_search<false, false>(C->wd_th, C->wd_ph, C->wd_gphi, C->wd_thpow, ap, ap, ap, 0, LS_WD, C->wd_ap,
+                                    T(-1));
+          flags = res_flags;
+          rejf |= (flags & LSR_REJF) != 0;
+          uth = C->wd_th;
+          uph = C->wd_ph;
+          if (flags & LSR_ACC) {
+            accepted = true;
+            C->in_wd = 0;
+            C->wd_short = 0;
+          } else if (++C->wd_trial <= MR_WD_TRIAL_MAX) {
+            take_anyway = true;  // the full step is taken tentatively (LS_WD stored that trial point already)
+          } else {
+            // back to the watchdog point: its iterate and direction, a regular backtracking line search
+            // that skips the full step
+            wd_restore();
+            C->in_wd = 0;
+            C->wd_short = 0;
+            th = C->wd_th; ph = C->wd_ph; gphi = C->wd_gphi; ap = C->wd_ap; ad = C->wd_ad; a_min = C->wd_amin;
+            th_pow = C->wd_thpow;
+            uth = th;
+            uph = ph;
+            line_search<false, false>(th, ph, gphi, th_pow, T(0.5) * ap, ap, a_min, 1, LS_NOSOC, T(0), T(-1));
             flags = res_flags;
             rejf |= (flags & LSR_REJF) != 0;
             accepted = (flags & LSR_ACC) != 0;
+          }
+        } else {
+          line_search<false, false>(th, ph, gphi, th_pow, ap, ap, a_min, 0, 0, T(0), T(-1));
+          flags = res_flags;
+          rejf |= (flags & LSR_REJF) != 0;
+          accepted = (flags & LSR_ACC) != 0;
+          if (flags & LSR_NEED_SOC) {
+            // IPOPT's TrySecondOrderCorrection: up to max_soc (4) linear corrections while theta falls by
+            // kappa_soc (0.99); then, if none is accepted, the backtracking resumes at alpha / 2
+            const T a_trial = res_alpha, a_test0 = res_atest;
+            T th_trial = res_th, a_soc = a_trial, th_old = T(0);
+            soc_prepare();
+            for (int count = 0; count < IP_MAX_SOC; ++count) {
+              if (count > 0 && !(th_trial <= T(IP_KAPPA_SOC) * th_old)) break;
+              th_old = th_trial;
+              if (count == 0)
+                line_search<false, false>(th, ph, gphi, th_pow, a_soc, ap, a_min, 0, LS_ACC, a_soc, a_soc);
+              else
+                line_search<false, true>(th, ph, gphi, th_pow, a_soc, ap, a_min, 0, LS_ACC, a_soc, a_soc);
+              MR_STAT(st_soc_try++);
+              MR_CNT(5);
+#if MR_PHASE_CYCLES
+              const unsigned long long ts0 = trace ? MR_CLOCK() : 0ull;
+#endif
+              soc_backward();
+#if MR_PHASE_CYCLES
+              const unsigned long long ts1 = trace ? MR_CLOCK() : 0ull;
+#endif
+              T aps, ads;
+              forward_soc(aps, ads);
+#if MR_PHASE_CYCLES
+              if (trace) { tsub[6] += ts1 - ts0; tsub[7] += MR_CLOCK() - ts1; }
+#endif
+              line_search<false, true>(th, ph, gphi, th_pow, aps, aps, aps, 0, LS_WD, a_test0, T(-1));
+              rejf |= (res_flags & LSR_REJF) != 0;
+              a_soc = aps;
+              if (!(res_flags & LSR_FIN)) break;
+              if (res_flags & LSR_ACC) {
+                soc_taken = accepted = true;
+                flags = res_flags;
+                ad = soc_commit();
+                break;
+              }
+              th_trial = res_th;
+            }
+            if (!soc_taken) {
+              line_search<false, false>(th, ph, gphi, th_pow, T(0.5) * a_trial, ap, a_min, 1, LS_NOSOC, T(0), T(-1));
+              flags = res_flags;
+              rejf |= (flags & LSR_REJF) != 0;
+              accepted = (flags & LSR_ACC) != 0;
+            }
+          }
+        }
+        if (MR_SOFT_RESTO && !accepted && !take_anyway) {
+          // IPOPT's soft restoration phase before the restoration phase proper (TrySoftRestoStep)
+          const int sr = soft_resto(th, ph, gphi, th_pow, ap, ad);
+          if (sr) {
+            accepted = soft_step = true;
+            soft_orig = sr == 1;
+            cw()->in_soft = soft_orig ? 0 : 1;
+            cw()->soft_count = 0;
+            uth = th;
+            uph = ph;
           }
         }
       }
@@ -2664,9 +3168,9 @@ struct WaveSolver {
       const int nls = res_nls;
       MR_STAT((st_trials += res_ntr, st_soc_ok += soc_taken, st_wd += take_anyway, st_lsfail += (!accepted && !take_anyway)));
       if (!accepted && !take_anyway) {
-        // IPOPT on a failed line search (the soft restoration phase is not restated): the
-        // current point acceptable -> "acceptable point reached"; almost feasible (theta <= 1e-2 tol) ->
-        // the stored acceptable point or restoration failed; otherwise the restoration phase
+        // IPOPT on a failed line search (and failed soft restoration): the current point acceptable ->
+        // "acceptable point reached"; almost feasible (theta <= 1e-2 tol) -> the stored acceptable point or
+        // restoration failed; otherwise the restoration phase
         if (acceptable(kkt)) { out.status = 1; break; }
         if (theta <= T(1e-2) * P.tol ||
             (sizeof(T) == 4 && mr_max(cw()->pr_eq, cw()->viol) <= T(IP_CONSTR_VIOL_TOL))) {  // fp32: feasible at its resolution
@@ -2691,7 +3195,7 @@ struct WaveSolver {
         }
         continue;
       }
-      if (!take_anyway) cw()->wd_short = (accepted && alpha < ap) ? cw()->wd_short + 1 : 0;
+      if (!take_anyway && !tiny && !soft_step) cw()->wd_short = (accepted && alpha < ap) ? cw()->wd_short + 1 : 0;
 #if MR_FILTER_RESET_TRIGGER > 0
       if (filt_resets < MR_MAX_FILTER_RESETS) {
         filt_rej_iters = rejf ? filt_rej_iters + 1 : 0;
@@ -2702,8 +3206,11 @@ struct WaveSolver {
         }
       }
 #endif
-      // IPOPT augments the filter unless the step is f-type with the Armijo condition
-      if (!take_anyway && (flags & LSR_AUG)) filter_add((T(1) - g_th) * uth, uph - g_ph * uth);
+      // IPOPT augments the filter unless the step is f-type with the Armijo condition (a tiny step: never; a
+      // soft restoration step: only when the regular criterion accepted it -- an h-type step)
+      if (!take_anyway && (soft_step ? soft_orig : (!tiny && (flags & LSR_AUG))))
+        filter_add((T(1) - g_th) * uth, uph - g_ph * uth);
+      if (soft_step) ad = alpha;  // the soft restoration step moves every variable by one step size
       if (trace && ln == 0 && it < trace_cap - 2) {
         double* tr = trace + 8 * it;
         tr[0] = (double)kkt; tr[1] = (double)mu; tr[2] = (double)alpha; tr[3] = (double)ad;

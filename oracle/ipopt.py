@@ -124,15 +124,16 @@ class Rules:
     resto_ls_mult: bool = True
     resto_watchdog: bool = True
     resto_soc: bool = True
+    resto_relax_x0: bool = True       # the initial-state rows S_0 = s0, X_0 = state0 relaxed in the restoration
+                                      # phase too (IPOPT relaxes every equality row; the product eliminates x_0)
     push_range_one_sided: bool = False  # round 3 pushed one-sided rows by min(1e-2 max(1,|b|), 1e-2 range)
 
 
 IPOPT = Rules()
-# the rules of the product (csrc/mr_solver.h, csrc/mr_wave.h): IPOPT's, without the soft restoration phase and
-# with the restoration phase's documented simplifications; the restoration phase's own iterates
-# are not compared (the product also keeps X_0 / S_0 hard and relaxes a two-sided row's distances separately)
-PRODUCT = replace(IPOPT, soft_resto=False, tiny_step=False, resto_ls_mult=False, resto_soc=False,
-                  resto_watchdog=False)
+# the rules of the product (csrc/mr_solver.h, csrc/mr_wave.h): IPOPT's, with the restoration phase's documented
+# simplifications; the restoration phase's own iterates are not compared (the product also keeps
+# X_0 / S_0 hard and relaxes a two-sided row's distances separately)
+PRODUCT = replace(IPOPT, resto_ls_mult=False, resto_soc=False, resto_watchdog=False, resto_relax_x0=False)
 R3 = Rules(opti_rows=False, bound_relax_factor=0.0, constr_scaling=False, ls_mult_init=False, separate_yd=False,
            sd_count_yd=False, kappa_d=0.0, delta_s=False, delta_inc_1e5=False, unscaled_tests=False, mu_floor="tol10",
            nlp_error_viol=False, max_soc=-1, ftype_rule="r3", first_trial=False, obj_max_inc=0.0, compare_eps=False,
@@ -151,8 +152,9 @@ class Problem:
     f, c, d: torch functions; lag_hess(x, wf, yc, yd) -> Hessian of wf f + yc.c + yd.d (numpy), optional;
     soc_roll(x) -> x with the shooting states re-simulated (round-3 SOC), optional."""
 
-    def __init__(self, n, f, c, d, dL, dU, xL=None, lag_hess=None, soc_roll=None, push=None):
+    def __init__(self, n, f, c, d, dL, dU, xL=None, lag_hess=None, soc_roll=None, push=None, x0_rows=0):
         self.n, self.f, self.c, self.d = n, f, c, d
+        self.x0_rows = x0_rows  # leading equality rows that fix the initial state (Rules.resto_relax_x0)
         self.dL, self.dU = np.asarray(dL, np.float64), np.asarray(dU, np.float64)
         self.xL = np.full(n, -np.inf) if xL is None else np.asarray(xL, np.float64)
         self.soc_roll, self.push = soc_roll, push
@@ -197,7 +199,7 @@ def _scaled(P, x0, rules):
     f, c, d, lh = P.f, P.c, P.d, P.lag_hess
     S = Problem(P.n, lambda x: df * f(x), lambda x: dct * c(x), lambda x: ddt * d(x), dd * P.dL, dd * P.dU, P.xL,
                 lag_hess=lambda x, wf, yc, yd: lh(x, wf * df, np.asarray(yc) * dc, np.asarray(yd) * dd),
-                soc_roll=P.soc_roll, push=P.push)
+                soc_roll=P.soc_roll, push=P.push, x0_rows=P.x0_rows)
     return S, df, dc, dd, max(mc, md)
 
 
@@ -664,9 +666,14 @@ class _Alg:
         mu_r = max(self.mu, E["pr_inf"])
         xR = it.x.copy()
         DR2 = np.minimum(1.0, 1.0 / np.maximum(np.abs(xR), 1e-300)) ** 2
-        pc, nc = _pn(ev["c"], mu_r, RHO)
+        rel = np.ones(mc, dtype=bool)  # the relaxed equality rows
+        if not R.resto_relax_x0:
+            rel[:P.x0_rows] = False
+        mr = int(rel.sum())
+        rel_t = torch.tensor(np.nonzero(rel)[0], dtype=torch.long)
+        pc, nc = _pn(ev["c"][rel], mu_r, RHO)
         pd, nd = _pn(ev["d"] - it.s, mu_r, RHO)
-        ia = np.cumsum([0, n, mc, mc, md, md])
+        ia = np.cumsum([0, n, mr, mr, md, md])
         zeta = [math.sqrt(mu_r)]
         xRt, DR2t = _T(xR), _T(DR2)
         f, c, d, lh = P.f, P.c, P.d, P.lag_hess
@@ -675,7 +682,7 @@ class _Alg:
             return RHO * torch.sum(v[n:]) + 0.5 * zeta[0] * torch.sum(DR2t * (v[:n] - xRt) ** 2)
 
         def cR(v):
-            return c(v[:n]) - v[ia[1]:ia[2]] + v[ia[2]:ia[3]]
+            return c(v[:n]).index_add(0, rel_t, -v[ia[1]:ia[2]] + v[ia[2]:ia[3]])
 
         def dR(v):
             return d(v[:n]) - v[ia[3]:ia[4]] + v[ia[4]:ia[5]]
@@ -1066,7 +1073,7 @@ def make_problem(prob, rules=IPOPT):
             ru = np.minimum(CONSTR_VIOL_TOL, bl * np.maximum(1.0, np.abs(dU)))
             dL = np.where(np.isfinite(dL), dL - rl, dL)
             dU = np.where(np.isfinite(dU), dU + ru, dU)
-        return Problem(n, prob.f, prob.g, d, dL, dU, soc_roll=prob.rollout)
+        return Problem(n, prob.f, prob.g, d, dL, dU, soc_roll=prob.rollout, x0_rows=7)  # g: S_0, X_0, dynamics
     mi = prob.push().size
     return Problem(n, prob.f, prob.g, prob.d, np.zeros(mi), np.full(mi, np.inf), soc_roll=prob.rollout,
                    push=prob.push())

@@ -1,0 +1,85 @@
+"""Generate tests/golden/c3_sample_ipopt.npz: the dense IPOPT restatement on a random sample of C3.
+
+TEST FIXTURE GENERATOR (build container only; the GPU box never runs the oracle's solves).
+
+C3 (dynamic model, hard lane rows of the commented control/MPC.py:135, t1_triple, N = 40, fp64) starts
+most instances outside the lane (the S_hat guess at top speed, MPC.py:127), so many solves enter IPOPT's
+restoration phase.  128 instances drawn uniformly from the 8 192-instance batch (numpy.random.default_rng(
+6003), stored as idx) are solved by oracle.ipopt.solve_ipopt at the parity tolerance of the C3 tests (tol
+1e-8, acceptable_tol 1e-6 over 15 iterations, max_iter 500) under the FULL IPOPT rules (``IPOPT``) and under
+the product's rules (``PRODUCT``: IPOPT's without the restoration phase's least-square multipliers, second-
+order corrections, watchdog and initial-state relaxation -- DESIGN.md §2).  Stored per rule set: status,
+iterations, restoration iterations, objective, U / X / S.  tests/test_gpu_golden.py compares the GPU with
+the IPOPT outcomes (status class on the sample, solutions where both solve); the PRODUCT columns are the
+audit of the remaining deviations (do they change outcomes?).
+
+Usage: python tests/golden/make_c3_sample_golden.py [--procs=8]
+"""
+import json
+import os
+import sys
+import time
+from multiprocessing import Pool
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.abspath(os.path.join(HERE, "..", ".."))
+sys.path.insert(0, os.path.join(REPO, "mpc-racing_amd"))
+sys.path.insert(0, REPO)
+
+N_INST = 128
+OPTIONS = dict(tol=1e-8, acceptable_tol=1e-6, acceptable_iter=15, max_iter=500)
+OUT = os.path.join(HERE, "c3_sample_ipopt.npz")
+RULES = ("IPOPT", "PRODUCT")
+
+
+def sample_indices():
+    return sorted(int(v) for v in np.random.default_rng(6003).choice(8192, N_INST, replace=False))
+
+
+def _solve(args):
+    import torch
+    torch.set_num_threads(1)
+    from mpcracing import workload as wl
+    from oracle import ipopt
+    from oracle.nlp import MPCProblem
+    j, rn = args
+    cfg = wl.CONFIGS["C3"]
+    b = wl.make_batch("C3", limit=j + 1)
+    inst = wl.instance_dicts(b)[j]
+    p = MPCProblem(inst["state0"], inst["s0"], inst["cx"], inst["cy"], inst["max_error"], N=cfg["N"], Ts=cfg["Ts"],
+                   model=cfg["model"], lane_bounds=cfg["lane"])
+    t0 = time.time()
+    r = ipopt.solve_ipopt(p, rules=getattr(ipopt, rn), log=True, **OPTIONS)
+    X, U, S, _eC, _eL = p.unpack(r.w)
+    return dict(status=r.status, iters=r.iters, resto_iters=sum(1 for e in r.log if e[7]), obj=r.obj, X=X, U=U,
+                S=S, why=r.why, stats=r.stats, t=time.time() - t0)
+
+
+def main():
+    procs = int(next((a.split("=")[1] for a in sys.argv[1:] if a.startswith("--procs=")), 8))
+    idx = sample_indices()
+    jobs = [(j, rn) for rn in RULES for j in idx]
+    with Pool(procs) as pool:
+        res = pool.map(_solve, jobs, chunksize=1)
+    out = {"idx": np.array(idx, dtype=np.int64)}
+    for rn in RULES:
+        rs = [r for (j, n), r in zip(jobs, res) if n == rn]
+        for k in ("X", "U", "S"):
+            out[f"{rn}_{k}"] = np.stack([r[k] for r in rs], axis=-1)
+        for k in ("status", "iters", "resto_iters"):
+            out[f"{rn}_{k}"] = np.array([r[k] for r in rs], dtype=np.int32)
+        out[f"{rn}_obj"] = np.array([r["obj"] for r in rs])
+        out[f"{rn}_why"] = np.array([r["why"] for r in rs])
+        print(json.dumps({"rules": rn, "n": len(rs), "options": OPTIONS,
+                          "status_counts": np.bincount(out[f"{rn}_status"], minlength=5).tolist(),
+                          "entered_restoration": int((out[f"{rn}_resto_iters"] > 0).sum()),
+                          "seconds": round(sum(r["t"] for r in rs), 1),
+                          "stats_total": {k: int(sum(r["stats"][k] for r in rs)) for k in rs[0]["stats"]}}),
+              flush=True)
+    np.savez_compressed(OUT, **out)
+
+
+if __name__ == "__main__":
+    main()

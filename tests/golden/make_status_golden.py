@@ -5,8 +5,10 @@ TEST FIXTURE GENERATOR (build container only; the GPU box never runs the oracle'
 The reference calls IPOPT with tol 1e-4, acceptable_tol 1e-2 (acceptable_iter: IPOPT's 15), max_iter 500
 (control/MPC.py:151-161, ControllerParameters.py:23).  SURVEY §8(c) lists the solver status class
 (converged / not converged) among the outputs that must match.  This script solves config 1 (the
-reference's script/test_mpc.py instance, dynamic and kinematic model) and the first 64 instances of C2, C4
-and C5 (mpcracing.workload.make_batch, deterministic) with oracle.ipopt.solve_ipopt under the FULL IPOPT
+reference's script/test_mpc.py instance, dynamic and kinematic model) and 64 instances of each of C2, C4 and
+C5 drawn uniformly from the per-GPU batch (mpcracing.workload.make_batch, deterministic; indices seeded
+numpy.random.default_rng(5000 + config#), stored as <config>_idx -- a spread sample, so the fixture's status
+fractions estimate the whole batch's) with oracle.ipopt.solve_ipopt under the FULL IPOPT
 rules (``ipopt.IPOPT``: soft restoration, tiny steps, the restoration phase's least-square multipliers,
 second-order corrections and watchdog included) in fp64 at exactly those options, and stores per instance
 the status (0 solved, 1 acceptable, 2 max_iter, 3 failed, 4 infeasible), the iteration count, why it
@@ -37,11 +39,20 @@ OPTIONS = dict(tol=1e-4, acceptable_tol=1e-2, acceptable_iter=15, max_iter=500)
 OUT = os.path.join(HERE, "status_ref_options.npz")
 
 
+def sample_indices(name):
+    """The fixture's instances of the per-GPU batch of config ``name`` (sorted)."""
+    from mpcracing import workload as wl
+    if name.startswith("C1"):
+        return [0]
+    B = wl.CONFIGS[name]["per_gpu"]
+    return sorted(int(v) for v in np.random.default_rng(5000 + int(name[1])).choice(B, N_INST, replace=False))
+
+
 def _config(name):
     from mpcracing import workload as wl
     if name.startswith("C1"):
         return dict(wl.CONFIGS["C1"], model=name[2:]), wl.make_batch("C1")
-    return wl.CONFIGS[name], wl.make_batch(name, limit=N_INST)
+    return wl.CONFIGS[name], wl.make_batch(name)
 
 
 def _n(name):
@@ -57,7 +68,8 @@ def _solve(args):
     name, i = args
     cfg, b = _config(name)
     tyres = wl.tyre_coeffs(cfg["tyres"]) if cfg["tyres"] else None
-    inst = wl.instance_dicts(b)[i]
+    j = sample_indices(name)[i]
+    inst = wl.instance_dicts({k: (v[..., j:j + 1] if v is not None else None) for k, v in b.items()})[0]
     p = MPCProblem(inst["state0"], inst["s0"], inst["cx"], inst["cy"], inst["max_error"], N=cfg["N"], Ts=cfg["Ts"],
                    model=cfg["model"], lane_bounds=cfg["lane"], tyres=tyres)
     t0 = time.time()
@@ -90,6 +102,7 @@ def main():
         for k in ("obj", "kkt", "viol"):
             out[f"{name}_{k}"] = np.array([r[k] for r in rs])
         out[f"{name}_why"] = np.array([r["why"] for r in rs])
+        out[f"{name}_idx"] = np.array(sample_indices(name), dtype=np.int64)
         summ = {"config": name, "n": _n(name), "options": OPTIONS, "rules": "IPOPT",
                 "status_counts": np.bincount(out[f"{name}_status"], minlength=5).tolist(),
                 "status": out[f"{name}_status"].tolist(), "iters": out[f"{name}_iters"].tolist(),

@@ -18,8 +18,8 @@ _lib = None
 
 def lib():
     global _lib
-    if _lib is None:
-        _lib = abi.load_host_twin()
+    if _lib is None:  # MR_HOST_TWIN_LIB: another host build of the source (developer A/B runs)
+        _lib = abi.load_host_twin(os.environ.get("MR_HOST_TWIN_LIB", abi.HOST_TWIN_LIB))
     return _lib
 
 
