@@ -745,7 +745,7 @@ struct SolveOut {
 // The line-search filter.  IPOPT's is unbounded; here it holds FCAP = FMAX + 64 FOVF entries, more than a
 // solve can add at max_iter <= 500 (at most one entry per iteration, the restoration phase's own filter
 // separate), so it never drops one there (the round-4 build kept the last 32, which the C3 audits showed
-// binding: 47-125 entries on long solves, profiles/r05_audit_C3_ipopt.json).  The wave kernel keeps the
+// binding: 47-196 entries on long solves, profiles/r05_audit_C3_ipopt.jsonl).  The wave kernel keeps the
 // first FMAX entries in LDS and the rest in the instance's cold fields (mr_wave.h CSF::FOV).
 #ifndef MR_FMAX
 #define MR_FMAX 32  // filter entries in LDS (wave kernel)

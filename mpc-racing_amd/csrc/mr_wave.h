@@ -73,7 +73,10 @@
 #define MR_RIC_AHEAD 2  // stages the Riccati's operand gathers run ahead of the factorisation (2 or 3)
 #endif
 #ifndef MR_MFMA_CHAIN
-#define MR_MFMA_CHAIN 1  // the forward / SOC recursions as MFMA products of the closed-loop map (0: lane-group dots)
+#define MR_MFMA_CHAIN 0  // 1: the forward / SOC recursions as MFMA products of the closed-loop map (A/B option: slower)
+#endif
+#ifndef MR_MFMA_SOCB
+#define MR_MFMA_SOCB 0  // the SOC costate pass as the transposed MFMA recursion (stage-parallel v_k: A/B option)
 #endif
 #ifndef MR_PRIO_ITER
 #define MR_PRIO_ITER 0  // > 0: the wave raises its issue priority (s_setprio) at this iteration
@@ -1485,7 +1488,10 @@ struct WaveSolver {
   };
   // TR: the transposed (costate) recursion, backward in k, v_k from the cold field SPV; SOCM: the affine
   // column from the SOC's cold fields (c_soc in SC, k_soc in SK0).  Result rows y to LDX[row k] (TR) or
-  // [row k + 1] (forward); the caller provides row 0 (forward: dx_0 = 0) or row N (TR: pv_N) in y0.
+  // [row k + 1] (forward); the caller provides the start y0 (forward: dx_0 = 0; TR: pv_N) as B-operand rows.
+  // The loop body only gathers (two stages ahead, three rotating register sets, exits at step ends: no
+  // register copies of in-flight loads), multiplies and writes LDS -- no global stores, whose completion
+  // the in-order vmcnt would make the next gather's wait include.
   template <bool TR, bool SOCM>
   MR_HD void mfma_chain(const T* y0) {
     const int N = wu(this->w, this->N), ln = this->ln;
@@ -1534,7 +1540,6 @@ struct WaveSolver {
     };
     // B operand: xb[s] = y[4s + g]
     T xb[4] = {y0[0], y0[1], y0[2], T(0)};
-    // output rows: lane (g, c = 0) holds D rows drow(g, v)
     const bool wr = (ln & 15) == 0;
     auto cstep = [&](int k, const ChainRaw& r) {
       T fr[3];
@@ -1561,41 +1566,133 @@ struct WaveSolver {
       for (int v = 0; v < 4; ++v) xb[v] = d[v];
       if constexpr (sizeof(T) == 4) wtranspose4(w, xb);
     };
+    // (scheduling barriers keep each prefetch ahead of the step that follows it: without them the
+    // scheduler sank the gathers to the back-edge and every step waited out a memory round trip)
     ChainRaw ra, rb2, rc2;
     if constexpr (!TR) {
       cload(0, ra);
       cload(1, rb2);
       for (int k = 0;; k += 3) {
-        if (k >= N) break;
         cload(k + 2, rc2);
+        MR_SCHED_BARRIER();
         cstep(k, ra);
-        if (k + 1 >= N) break;
+        if (k + 1 == N) break;
         cload(k + 3, ra);
+        MR_SCHED_BARRIER();
         cstep(k + 1, rb2);
-        if (k + 2 >= N) break;
+        if (k + 2 == N) break;
         cload(k + 4, rb2);
+        MR_SCHED_BARRIER();
         cstep(k + 2, rc2);
+        if (k + 3 == N) break;
       }
     } else {
       cload(N - 1, ra);
       cload(N - 2, rb2);
       for (int k = N - 1;; k -= 3) {
-        if (k < 0) break;
         cload(k - 2, rc2);
+        MR_SCHED_BARRIER();
         cstep(k, ra);
-        if (k - 1 < 0) break;
+        if (k == 0) break;
         cload(k - 3, ra);
+        MR_SCHED_BARRIER();
         cstep(k - 1, rb2);
-        if (k - 2 < 0) break;
+        if (k == 1) break;
         cload(k - 4, rb2);
+        MR_SCHED_BARRIER();
         cstep(k - 2, rc2);
+        if (k == 2) break;
       }
     }
     wsync_lds(w);
   }
 
-  // the forward substitution by mfma_chain, then stage-parallel: du_k = K_k dx_k + kff_k, the costate step
-  // dnu_k = P_k dx_k + p_k (SOCM: the SOC's kff and costate vector, into SDNU)
+  // After the forward recursion (dx_k in LDX rows): per stage, independent of the others, the product
+  // G_k [dx_k; 1] with G_k = [P_k | p_k ; K_k | kff_k] (rows 0..10: the costate step dnu_k; rows 11..13: du_k;
+  // SOCM: the SOC's costate vector and k_soc from the cold fields), on the MFMA with the same lane maps;
+  // every lane gathers from the same stage record (a few cache lines per gather), two stages ahead.
+  // dnu_k to its stage field (SSF::DNU; SOCM: the cold SDNU), du_k to LDS (LX_OFF + 3 k + a).
+  template <bool SOCM>
+  MR_HD void gpass() {
+    const int N = wu(this->w, this->N), ln = this->ln;
+    const Wv w = this->w;
+    const WBuf<T> wb(rc - (int64_t)SSF::NF * WL, (unsigned)WS_NU_OFF);
+    auto R = [](int k) { return (unsigned)(SSF::NF * WL) + (unsigned)k * (unsigned)RC_STRIDE; };
+    const unsigned cold0 = (unsigned)(SSF::NF * WL) + (unsigned)RC_STRIDE * WL;
+    MR_LDS T* const LDX = lds + LDX_OFF;
+    const int i = ln & 15, g = ln >> 4;
+    unsigned goff[3], xoff[3];
+    for (int s = 0; s < 3; ++s) {
+      const int j = 4 * s + g;
+      goff[s] = (i < NX) ? (j < NX ? (unsigned)(RCF::P + pidx(i, j)) : (j == 11 ? (unsigned)(RCF::PV0 + i) : (unsigned)RCF::CZERO))
+                         : (i < NX + NU ? (j < NX ? (unsigned)(RCF::K + (i - NX) * NX + j)
+                                                  : (j == 11 ? (unsigned)(RCF::K0 + i - NX) : (unsigned)RCF::CZERO))
+                                        : (unsigned)RCF::CZERO);
+      xoff[s] = (unsigned)j;  // B operand row j of y_k = [dx_k; 1] (LDX row k, element 11 set below)
+    }
+    const bool gaff = SOCM && g == 3 && i < NX + NU;  // G's affine column from the SOC's cold fields
+    const unsigned gcoff = gaff ? (unsigned)((i < NX ? CSF::SPV + i : CSF::SK0 + i - NX) * WL) : (unsigned)CSF::SJUNK * WL;
+    struct GRaw {
+      T q[3], c;
+    };
+    auto gload = [&](int kk, GRaw& r) {
+      kk = kk < N ? kk : N;
+      const unsigned ro = (unsigned)wu(w, (int)R(kk));
+#pragma unroll
+      for (int s = 0; s < 3; ++s) r.q[s] = wb.ld(ro, goff[s]);
+      if constexpr (SOCM) r.c = wb.ld((unsigned)wu(w, (int)(cold0 + (unsigned)kk)), gcoff);
+    };
+    const bool wr = (ln & 15) == 0;
+    auto gstep = [&](int k, const GRaw& r) {
+      T gf[3] = {r.q[0], r.q[1], r.q[2]};
+      if constexpr (SOCM) gf[2] = gaff ? r.c : gf[2];
+      T xb[3];
+#pragma unroll
+      for (int s = 0; s < 3; ++s) xb[s] = xoff[s] < 11 ? LDX[k * 12 + xoff[s]] : (xoff[s] == 11 ? T(1) : T(0));
+      T e[4] = {T(0), T(0), T(0), T(0)}, e2[4] = {T(0), T(0), T(0), T(0)};
+      wmfma(w, gf[0], xb[0], e);
+      wmfma(w, gf[2], xb[2], e2);
+      wmfma(w, gf[1], xb[1], e);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) e[v] += e2[v];
+      const bool dn = k >= 1 || !MR_KKT_RESTATED;  // k = 0: the initial-state rows' multiplier step
+      const unsigned ku = (unsigned)wu(w, k), junk = R(k) + RCF::JUNK - ku;  // (stage k's record discard slot)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int row = drow(g, v);
+        const bool st = wr && row < NX && dn;
+        if constexpr (SOCM) {
+          wb.st(e[v], ku, st ? cold0 + (unsigned)(CSF::SDNU + row) * WL : junk);
+        } else if constexpr (SSL) {
+          if (st) ss[(SSF::DNU + row) * WL + k] = e[v];
+        } else {  // branch-free: other lanes write the discard slot
+          wb.st(e[v], ku, st ? (unsigned)(SSF::DNU + row) * WL : junk);
+        }
+        lds[(wr && row >= NX && row < NX + NU && k < N) ? LX_OFF + 3 * k + row - NX : LJUNK_OFF + ln] = e[v];
+      }
+    };
+    GRaw ga, gb, gc;
+    gload(0, ga);
+    gload(1, gb);
+    for (int k = 0;; k += 3) {
+      gload(k + 2, gc);
+      MR_SCHED_BARRIER();
+      gstep(k, ga);
+      if (k == N) break;
+      gload(k + 3, ga);
+      MR_SCHED_BARRIER();
+      gstep(k + 1, gb);
+      if (k + 1 == N) break;
+      gload(k + 4, gb);
+      MR_SCHED_BARRIER();
+      gstep(k + 2, gc);
+      if (k + 2 == N) break;
+    }
+    wsync_lds(w);
+  }
+
+  // the forward substitution by mfma_chain (dx_k to LDX rows), then gpass (dnu_k to its field, du_k to LDS),
+  // then this lane's stage direction dz (SOCM: the SOC's kff / costate vector, dnu into SDNU)
   template <bool SOCM>
   MR_HD void fwd_chain(T* dz) {
     const int N = wu(this->w, this->N);
@@ -1605,25 +1702,11 @@ struct WaveSolver {
     for (int s = 0; s < 3; ++s) y0[s] = (4 * s + g == 11) ? T(1) : T(0);
     if (ln < 12) LDX[ln] = T(0);  // dx_0 = 0
     mfma_chain<false, SOCM>(y0);
-    if (ln <= N) {
-      const int k = ln;
-      const MR_GLOBAL T* Rk = R(k);
-      T dx[NX];
-      for (int j = 0; j < NX; ++j) { dx[j] = LDX[k * 12 + j]; dz[j] = dx[j]; }
-      if (k < N)
-        for (int a = 0; a < NU; ++a) {
-          T v = SOCM ? Cf(CSF::SK0 + a) : Rk[RCF::K0 + a];
-          for (int j = 0; j < NX; ++j) v += Rk[RCF::K + a * NX + j] * dx[j];
-          dz[NX + a] = v;
-        }
-      for (int r = 0; r < NX; ++r) {
-        T v = SOCM ? Cf(CSF::SPV + r) : Rk[RCF::PV0 + r];
-        for (int j = 0; j < NX; ++j) v += Rk[RCF::P + pidx(r, j)] * dx[j];
-        if (k >= 1 || !MR_KKT_RESTATED) {  // k = 0: the initial-state rows' multiplier step
-          if constexpr (SOCM) Cf(CSF::SDNU + r) = v; else S(SSF::DNU + r) = v;
-        }
-      }
-    }
+    gpass<SOCM>();
+    if (ln <= N)
+      for (int j = 0; j < NX; ++j) dz[j] = LDX[ln * 12 + j];
+    if (ln < N)
+      for (int a = 0; a < NU; ++a) dz[NX + a] = lds[LX_OFF + 3 * ln + a];
   }
 
   // ---------------- sweep 3: forward substitution, slack/dual steps ----------------
@@ -2175,7 +2258,7 @@ struct WaveSolver {
       for (int i = 0; i < NZ; ++i) Cf(CSF::SG + i) = g[i];
     }
     wsync(w);
-#if MR_MFMA_CHAIN
+#if MR_MFMA_SOCB
     // pv_k = Acl_k^T pv_{k+1} + v_k with v_k = A_k^T q + K_k^T u_k + g_x, q = P_{k+1} c_k, u_k = B_k^T q + g_u
     // (then r_k = B_k^T pv_{k+1} + u_k): v_k, u_k stage-parallel into the cold fields SPV / SK0, the
     // recursion by mfma_chain<TR>, then r_k and the feed-forward stage-parallel

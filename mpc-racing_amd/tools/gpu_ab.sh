@@ -1,0 +1,15 @@
+#!/bin/bash
+# A/B of library variants on the C4 bench line: for each given .so (MR_PRODUCT_LIB), bench.py without the
+# CPU baseline, 3 timed steps; lines to gpurun_out/<tag>_ab_<name>.json.  Stops at the first crash/timeout.
+# Usage: gpu_ab.sh TAG lib1.so lib2.so ...
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+mkdir -p gpurun_out
+TAG=$1; shift
+for lib in "$@"; do
+  n=$(basename "$lib" .so)
+  MR_PRODUCT_LIB=$lib timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --pipeline 0 > gpurun_out/${TAG}_ab_$n.json 2> gpurun_out/${TAG}_ab_$n.err
+  rc=$?
+  echo "$n rc=$rc" >> gpurun_out/${TAG}_ab.log
+  if [ $rc -ne 0 ]; then exit $rc; fi
+done

@@ -23,9 +23,23 @@ from mpcracing.batch import solver_for_config  # noqa: E402
 NAMES = ["eval", "riccati", "forward", "trial", "n_trials", "n_soc_tries", "n_fact", "total"]
 
 
+def _solver(name, B):
+    """AGENT: the reference agent's call (agent.py:154,171-183; bench.py agent_call): N = 15, dynamic model,
+    fp64, Ts 0.05, the reference's IPOPT options, on C2 instances."""
+    if name == "AGENT":
+        from mpcracing.batch import BatchSolver
+        return BatchSolver(15, "dyn", "fp64", False, 0.05, max_batch=B, tol=1e-4, acceptable_tol=1e-2,
+                           acceptable_iter=15)
+    return solver_for_config(name, B)
+
+
+def _batch(name):
+    return wl.make_batch("C2", limit=100) if name == "AGENT" else wl.make_batch(name)
+
+
 def one(name, b, i, cap=520):
     sub = {k: (v[..., i:i + 1].copy() if v is not None else None) for k, v in b.items()}
-    s = solver_for_config(name, 1)
+    s = _solver(name, 1)
     out = s.solve(sub, trace_instance=0, trace_cap=cap)
     torch.cuda.synchronize()
     lat = []
@@ -51,9 +65,9 @@ def main():
     names = sys.argv[1].split(",") if len(sys.argv) > 1 else ["C4"]
     res = {}
     for name in names:
-        b = wl.make_batch(name)
+        b = _batch(name)
         B = b["s0"].shape[0]
-        s = solver_for_config(name, B)
+        s = _solver(name, B)
         o = {k: v.cpu().numpy() for k, v in s.solve(b).items()}
         it = o["iters"]
         order = np.argsort(it)
