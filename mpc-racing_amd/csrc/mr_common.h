@@ -60,7 +60,14 @@ MR_HD float mr_atan2(float y, float x) { return atan2f(y, x); }
 MR_HD float mr_atan(float a) { return atanf(a); }
 MR_HD float mr_sqrt(float a) { return sqrtf(a); }
 MR_HD float mr_exp(float a) { return expf(a); }
+#if MR_DEVICE_BUILD
+// fp32 ln on the device: the hardware log2 (v_log_f32) times ln 2 -- 2 instructions against the library's
+// 8 (its extended-precision ln 2 product and infinity guard); a ~2 ulp result for the barrier terms
+// (fp32 solves only; -inf at 0 and NaN below, as logf)
+MR_HD float mr_log(float a) { return __builtin_amdgcn_logf(a) * 0.69314718055994531f; }
+#else
 MR_HD float mr_log(float a) { return logf(a); }
+#endif
 MR_HD float mr_abs(float a) { return fabsf(a); }
 
 // 1/sqrt(a), a > 0: IEEE in fp64 and on the host; the hardware v_rsq_f32 (1 ulp) on the device

@@ -581,7 +581,7 @@ struct WaveSolver {
       for (int i = 0; i < NX; ++i)
         if (i < 6 || (k == 0 && i == 6)) ok_l &= mr_abs(S(SSF::DNU + i)) <= big ? 1 : 0;
     }
-    const bool ok = wmin(w, ok_l) != 0;
+    const bool ok = wall(w, ok_l != 0);
     if (own()) {
       for (int i = 0; i < NX; ++i) {
         NUd(i) = ok ? (double)S(SSF::DNU + i) : 0.0;
@@ -2087,7 +2087,7 @@ struct WaveSolver {
       }
       th_t = wsum(w, th_l);
       const T fv = wsum(w, f_l), lg = wsum(w, lg_l), lin = wsum(w, lin_l);
-      int ok = wmin(w, ok_l);
+      int ok = wall(w, ok_l != 0) ? 1 : 0;
       ph_t = fv - mu * lg + kdm * lin;
       if constexpr (RESTO) {
         ph_t = fv - mu * (lg + wsum(w, lgr_l)) + kdm * lin;
@@ -2504,11 +2504,15 @@ struct WaveSolver {
       const T a = Cf(CSF::FOV + (2 * bank) * FOVF + q), b = Cf(CSF::FOV + (2 * bank + 1) * FOVF + q);
       hit |= (base + ln < n && th >= a && ph >= b) ? 1 : 0;
     }
-    return wmax(w, hit) != 0;
+    return wany(w, hit != 0);
+  }
+  // entry i of the LDS bank tested by lane i (th, ph wave-uniform)
+  MR_HD bool filter_hit_lds(T th, T ph, int n, const MR_LDS T* fth0, const MR_LDS T* fph0) const {
+    const int i = ln < FMAX ? ln : FMAX - 1;
+    return wany(w, ln < n && ln < FMAX && th >= fth0[i] && ph >= fph0[i]);
   }
   MR_HD bool filter_ok(T th, T ph) const {
-    for (int i = 0; i < FMAX; ++i)
-      if (i < nfilt && th >= fth(i) && ph >= fph(i)) return false;
+    if (filter_hit_lds(th, ph, nfilt, &fth(0), &fph(0))) return false;
     if (nfilt > FMAX && filter_hit_ov(th, ph, nfilt, fbank())) return false;
     return true;
   }
@@ -2654,8 +2658,7 @@ struct WaveSolver {
     auto* C = cw();
     const T tho = C->tho, pho = C->pho;
     bool ok = tho <= T(RESTO_KAPPA) * C->th_entry;
-    for (int i = 0; i < FMAX; ++i)
-      if (i < C->onfilt && tho >= C->ofilt[i] && pho >= C->ofilt[FMAX + i]) ok = false;
+    if (filter_hit_lds(tho, pho, C->onfilt, &C->ofilt[0], &C->ofilt[FMAX])) ok = false;
     if (C->onfilt > FMAX && filter_hit_ov(tho, pho, C->onfilt, 0)) ok = false;  // the original filter's bank
     return wuni(w, ok);
   }
@@ -2921,7 +2924,7 @@ struct WaveSolver {
       for (int i = 0; i < NX; ++i)
         if ((i < 6 || (k == 0 && i == 6)) && !(mr_abs(S(SSF::DNU + i)) < T(1e-2))) ys_l = 0;
     }
-    const int t = wmin(w, tiny_l), y = wmin(w, ys_l);
+    const int t = wall(w, tiny_l != 0), y = wall(w, ys_l != 0);
     res_flags = (t ? 1 : 0) | (y ? 2 : 0);
   }
 

@@ -126,6 +126,9 @@ __device__ __forceinline__ void wmfma(const Wv&, double a, double b, double* d) 
 // A condition every lane computed identically, made visibly wave-uniform (SGPR) so branches
 // on it stay scalar and the enclosing loop keeps a uniform counter and exact waitcnts.
 __device__ __forceinline__ bool wuni(const Wv&, bool b) { return __builtin_amdgcn_readfirstlane((int)b) != 0; }
+// any / every lane of the wave (one v_cmp into a lane mask; called in wave-uniform control flow)
+__device__ __forceinline__ bool wany(const Wv&, bool b) { return __builtin_amdgcn_ballot_w64(b) != 0; }
+__device__ __forceinline__ bool wall(const Wv&, bool b) { return __builtin_amdgcn_ballot_w64(!b) == 0; }
 // A value every lane holds identically (e.g. reloaded from the per-lane solver object): SGPR copy
 __device__ __forceinline__ int wu(const Wv&, int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ float wu(const Wv&, float v) {
@@ -409,6 +412,8 @@ template <typename T>
 inline T wmax(const Wv& w, T v) { return host_butterfly(w, v, [](T a, T b) { return b > a ? b : a; }); }
 template <typename T>
 inline T wmin(const Wv& w, T v) { return host_butterfly(w, v, [](T a, T b) { return b < a ? b : a; }); }
+inline bool wany(const Wv& w, bool b) { return wmax(w, b ? 1 : 0) != 0; }
+inline bool wall(const Wv& w, bool b) { return wmin(w, b ? 1 : 0) != 0; }
 
 // Run body(hw, lane, arg) as 64 fibers to completion.
 inline void host_wave_run(HostWave& hw, void (*body)(HostWave*, int, void*), void* arg) {
