@@ -76,7 +76,7 @@
 #define MR_MFMA_CHAIN 0  // 1: the forward / SOC recursions as MFMA products of the closed-loop map (A/B option: slower)
 #endif
 #ifndef MR_MFMA_SOCB
-#define MR_MFMA_SOCB 0  // the SOC costate pass as the transposed MFMA recursion (stage-parallel v_k: A/B option)
+#define MR_MFMA_SOCB 2  // the SOC costate pass on stage-parallel v_k, u_k: 2 the lean lane recursion (socb_chain), 1 the MFMA chain (A/B option), 0 the lane-group recursion
 #endif
 #ifndef MR_PRIO_ITER
 #define MR_PRIO_ITER 0  // > 0: the wave raises its issue priority (s_setprio) at this iteration
@@ -309,7 +309,7 @@ struct WaveSolver {
   double* trace = nullptr;
   int trace_cap = 0;
 #if MR_PHASE_CYCLES
-  unsigned long long tsub[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // diagnostics: sub-phase cycles of the trace instance
+  unsigned long long tsub[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // diagnostics: sub-phase cycles of the trace instance
 #endif
 
   MR_HD WaveSolver(const MR_CONST ProbParams<T>& P_, const Inst<T>& I_, Wv w_, MR_GLOBAL T* ws, MR_LDS T* lds_,
@@ -333,7 +333,10 @@ struct WaveSolver {
   MR_HD int nxt() const { return (ln + 1) & (WL - 1); }
 
   MR_HD void load_z(int b, T* z) const {
-    for (int i = 0; i < NZS; ++i) z[i] = own() ? S(zf(b) + i) : T(0);
+    for (int i = 0; i < NZS; ++i) {
+      const T v = S(zf(b) + i);  // (unconditional: all loads in flight together)
+      z[i] = own() ? v : T(0);
+    }
     if (ln >= N) { z[11] = T(0); z[12] = T(0); z[13] = T(0); }
   }
 
@@ -1973,12 +1976,25 @@ struct WaveSolver {
                             T acc) {
     MR_UNIFORM_P();
     MR_ASSUME_LDS_STATE();
+#if MR_PHASE_CYCLES
+    const unsigned long long tls0 = trace ? MR_CLOCK() : 0ull;
+#endif
     const int nb = 1 - cur;
     const int k = ln;
     const int N = wu(w, this->N);
     T z[NZS], dz[NZS], s_c[NI], ds[NI];
+    // every operand loaded unconditionally (every lane's fields exist), then selected: one memory round
+    // trip for the whole set instead of masked loads, each waited for in its branch
     load_z(cur, z);
-    for (int i = 0; i < NZS; ++i) dz[i] = own() ? (SOCDIR ? Cf(CSF::SDZ + i) : S(SSF::DZ + i)) : T(0);
+    for (int i = 0; i < NZS; ++i) {
+      const T v = SOCDIR ? Cf(CSF::SDZ + i) : S(SSF::DZ + i);
+      dz[i] = own() ? v : T(0);
+    }
+    T sv[NI], dv[NI];
+    for (int j = 0; j < NI; ++j) {
+      sv[j] = S(sf(cur) + j);
+      dv[j] = SOCDIR ? Cf(CSF::SDS + j) : S(SSF::DS + j);
+    }
     unsigned actm = 0u;  // active rows of this stage (depend on the stage only, not on the point)
 #pragma unroll
     for (int r = 0; r < NROW; ++r) {
@@ -1990,8 +2006,8 @@ struct WaveSolver {
     actm |= (own() && lane_active(P, k)) ? (3u << JL) : 0u;
     for (int j = 0; j < NI; ++j) {
       const bool a = (actm >> j) & 1u;
-      s_c[j] = a ? S(sf(cur) + j) : T(1);
-      ds[j] = a ? (SOCDIR ? Cf(CSF::SDS + j) : S(SSF::DS + j)) : T(0);
+      s_c[j] = a ? sv[j] : T(1);
+      ds[j] = a ? dv[j] : T(0);
     }
     // restoration: the relaxations and their steps (rows of this stage; vehicle rows of x_{k+1})
     T rp[NI], rn[NI], rdp[NI], rdn[NI], cp[6], cn[6], cdp[6], cdn[6], zr[NZS];
@@ -2002,25 +2018,33 @@ struct WaveSolver {
       mu_o = cw()->mu_o;
       for (int j = 0; j < NI; ++j) {
         const bool a = (actm >> j) & 1u;
-        rp[j] = a ? Cf(CSF::RP + j) : T(1);
-        rn[j] = a ? Cf(CSF::RN + j) : T(1);
-        rdp[j] = a ? Cf(CSF::RDP + j) : T(0);
-        rdn[j] = a ? Cf(CSF::RDN + j) : T(0);
+        const T v0 = Cf(CSF::RP + j), v1 = Cf(CSF::RN + j), v2 = Cf(CSF::RDP + j), v3 = Cf(CSF::RDN + j);
+        rp[j] = a ? v0 : T(1);
+        rn[j] = a ? v1 : T(1);
+        rdp[j] = a ? v2 : T(0);
+        rdn[j] = a ? v3 : T(0);
       }
       const bool dk = own() && k < N;
       for (int i = 0; i < 6; ++i) {
-        cp[i] = dk ? Cf(CSF::CP + i) : T(1);
-        cn[i] = dk ? Cf(CSF::CN + i) : T(1);
-        cdp[i] = dk ? Cf(CSF::CDP + i) : T(0);
-        cdn[i] = dk ? Cf(CSF::CDN + i) : T(0);
+        const T v0 = Cf(CSF::CP + i), v1 = Cf(CSF::CN + i), v2 = Cf(CSF::CDP + i), v3 = Cf(CSF::CDN + i);
+        cp[i] = dk ? v0 : T(1);
+        cn[i] = dk ? v1 : T(1);
+        cdp[i] = dk ? v2 : T(0);
+        cdn[i] = dk ? v3 : T(0);
       }
-      for (int i = 0; i < NZS; ++i) zr[i] = own() ? Cf(CSF::RZ + i) : T(0);
+      for (int i = 0; i < NZS; ++i) {
+        const T v = Cf(CSF::RZ + i);
+        zr[i] = own() ? v : T(0);
+      }
     }
     T zt[NZS], st[NI];
     const T kdm = T(IP_KAPPA_D) * mu;
     // one trial point: zt, st (registers), theta, phi; false if a slack is not positive or a value is
     // not finite.  accum: add its constraint values to the SOC right-hand sides (SC, SR)
     auto eval = [&](T alpha, bool accum, T& th_t, T& ph_t) -> bool {
+#if MR_PHASE_CYCLES
+      const unsigned long long te0 = trace ? MR_CLOCK() : 0ull;
+#endif
       for (int i = 0; i < NZS; ++i) zt[i] = z[i] + alpha * dz[i];
       if (k == 0)
         for (int i = 0; i < NX; ++i) zt[i] = z[i];  // x_0 fixed
@@ -2085,9 +2109,15 @@ struct WaveSolver {
           }
         }
       }
+#if MR_PHASE_CYCLES
+      const unsigned long long te1 = trace ? MR_CLOCK() : 0ull;
+#endif
       th_t = wsum(w, th_l);
       const T fv = wsum(w, f_l), lg = wsum(w, lg_l), lin = wsum(w, lin_l);
       int ok = wall(w, ok_l != 0) ? 1 : 0;
+#if MR_PHASE_CYCLES
+      if (trace) { tsub[8] += te1 - te0; tsub[9] += MR_CLOCK() - te1; }
+#endif
       ph_t = fv - mu * lg + kdm * lin;
       if constexpr (RESTO) {
         ph_t = fv - mu * (lg + wsum(w, lgr_l)) + kdm * lin;
@@ -2097,6 +2127,9 @@ struct WaveSolver {
       if (!(th_t == th_t) || !(ph_t == ph_t)) ok = 0;
       return wuni(w, ok != 0);
     };
+#if MR_PHASE_CYCLES
+    if (trace) tsub[11] += MR_CLOCK() - tls0;
+#endif
     const LSRef<T> ref{th, ph, gphi, th_pow};
     T alpha = a0, ph_acc = ph, a_test = a0, th_t = T(0), ph_t = T(0);
     int nls = nls0, ntr = 0;
@@ -2115,6 +2148,9 @@ struct WaveSolver {
         a_test = (mode & LS_WD) ? a_fix : alpha;
         const bool fin = eval(alpha, false, th_t, ph_t);
         ntr++;
+#if MR_PHASE_CYCLES
+        const unsigned long long ta0 = trace ? MR_CLOCK() : 0ull;
+#endif
         bool ok = false;
         if (fin) {
           ok = th_t <= theta_max;
@@ -2124,6 +2160,9 @@ struct WaveSolver {
           }
           if (ok && !filter_ok(th_t, ph_t)) { ok = false; flags |= LSR_REJF; }
         }
+#if MR_PHASE_CYCLES
+        if (trace) tsub[10] += MR_CLOCK() - ta0;
+#endif
         if (wuni(w, ok)) {
           flags |= LSR_ACC | LSR_FIN;
           if (!(is_ftype(a_test, ref) && armijo(ph_t, a_test, ref))) flags |= LSR_AUG;
@@ -2214,6 +2253,104 @@ struct WaveSolver {
     }
     wsync(w);
   }
+  // The SOC costate recursion given v_k, u_k (cold fields SPV, SK0: everything that does not depend on
+  // pv_{k+1}): lane i < NX forms pv_k[i] = v_k[i] + (A_k^T pv_{k+1})[i] + sum_a K_k[a][i] (B_k^T pv_{k+1})[a]
+  // from pv_{k+1} broadcast by v_readlane; B_k^T pv_{k+1} (the same in every lane) plus u_k is r_k, the
+  // feed-forward's right-hand side.  Results to LDS only (pv_k to LDX row k, r_k to [LX_OFF + 3 k]): no
+  // global stores in the loop, so the in-order vmcnt waits for the prefetched operands stay exact.  Per
+  // stage: one broadcast of pv (11 v_readlane), ~25 FMAs, 23 buffer loads issued three stages ahead.
+  MR_HD void socb_chain() {
+    const int N = wu(this->w, this->N), ln = this->ln;
+    const Wv w = this->w;
+    const WBuf<T> wb(rc - (int64_t)SSF::NF * WL, (unsigned)WS_NU_OFF);
+    auto R = [](int k) { return (unsigned)(SSF::NF * WL) + (unsigned)k * (unsigned)RC_STRIDE; };
+    const unsigned cold0 = (unsigned)(SSF::NF * WL) + (unsigned)RC_STRIDE * WL;
+    MR_LDS T* const LDX = lds + LDX_OFF;
+    const bool row = ln < NX;
+    const int li = row ? ln : 0;
+    // per-lane operand offsets: column li of A (vehicle rows: J[j][li], li < 6), column li of K, v_k[li];
+    // the shared J[j][6 + a] (B's vehicle rows) and u_k are the same address in every lane
+    unsigned aoff[6], koff[NU];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) aoff[j] = li < 6 ? (unsigned)(RCF::J + j * 8 + li) : (unsigned)RCF::CZERO;
+#pragma unroll
+    for (int a = 0; a < NU; ++a) koff[a] = (unsigned)(RCF::K + a * NX + li);
+    const int lr = ln < NU ? ln : 0;
+    const unsigned voff = (unsigned)(CSF::SPV + li) * WL, uoff = (unsigned)(CSF::SK0 + lr) * WL;
+    struct Ops {
+      T acol[6], kcol[NU], v, jb[12], u;
+    };
+    auto ld = [&](int k, Ops& o) {
+      const unsigned rk = (unsigned)wu(w, (int)R(k));
+#pragma unroll
+      for (int j = 0; j < 6; ++j) o.acol[j] = wb.ld(rk, aoff[j]);
+#pragma unroll
+      for (int a = 0; a < NU; ++a) o.kcol[a] = wb.ld(rk, koff[a]);
+      o.v = wb.ld(cold0 + (unsigned)k, voff);
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        o.jb[2 * j] = wb.ld(rk, (unsigned)(RCF::J + j * 8 + 6));
+        o.jb[2 * j + 1] = wb.ld(rk, (unsigned)(RCF::J + j * 8 + 7));
+      }
+      o.u = wb.ld(cold0 + (unsigned)k, uoff);  // lane a < NU: u_k[a]
+    };
+    T pv = wb.ld(cold0 + (unsigned)N, (unsigned)(CSF::SG + li) * WL);  // pv_N = g_x,N
+    LDX[row ? N * 12 + ln : LJUNK_OFF - LDX_OFF + ln] = pv;
+    auto step = [&](int k, const Ops& o) {
+      T p[NX];
+      wgather<T, NX>(w, pv, p);
+      // B^T pv (mr_solver.h apply_Bt): every lane the same three values
+      T b0 = p[7], b1 = p[8], c0 = T(0), c1 = T(0);
+      if (k == 0) { b0 += p[9]; b1 += p[10]; }
+#pragma unroll
+      for (int j = 0; j < 6; j += 2) {
+        b0 += o.jb[2 * j] * p[j];
+        b1 += o.jb[2 * j + 1] * p[j];
+        c0 += o.jb[2 * j + 2] * p[j + 1];
+        c1 += o.jb[2 * j + 3] * p[j + 1];
+      }
+      b0 += c0;
+      b1 += c1;
+      const T b2 = p[6];
+      // (A^T pv)[li] (mr_solver.h apply_At): the vehicle columns from J, the structural ones selected
+      T at0 = o.acol[0] * p[0], at1 = o.acol[1] * p[1];
+      at0 += o.acol[2] * p[2];
+      at1 += o.acol[3] * p[3];
+      at0 += o.acol[4] * p[4];
+      at1 += o.acol[5] * p[5];
+      const T sx = ln == 6 ? p[6] : ((k > 0 && ln == 9) ? p[9] : ((k > 0 && ln == 10) ? p[10] : T(0)));
+      const T at = ln < 6 ? at0 + at1 : sx;
+      pv = o.v + at + o.kcol[0] * b0 + o.kcol[1] * b1 + o.kcol[2] * b2;
+      LDX[row ? k * 12 + ln : LJUNK_OFF - LDX_OFF + ln] = pv;
+      const T bt = lr == 0 ? b0 : (lr == 1 ? b1 : b2);
+      lds[ln < NU ? LX_OFF + 3 * k + ln : LJUNK_OFF + ln] = bt + o.u;  // r_k
+    };
+    // operands three stages ahead, four rotating sets (unrolled by four: no register copies of in-flight
+    // loads); a prefetch past stage 0 re-reads stage 0 (unconditional loads, exact waits)
+    if (N > 0) {
+      auto kc = [](int k) { return k > 0 ? k : 0; };
+      Ops b0, b1, b2, b3;
+      ld(N - 1, b0);
+      ld(kc(N - 2), b1);
+      ld(kc(N - 3), b2);
+      for (int k = N - 1;; k -= 4) {
+        ld(kc(k - 3), b3);
+        step(k, b0);
+        if (k == 0) break;
+        ld(kc(k - 4), b0);
+        step(k - 1, b1);
+        if (k == 1) break;
+        ld(kc(k - 5), b1);
+        step(k - 2, b2);
+        if (k == 2) break;
+        ld(kc(k - 6), b2);
+        step(k - 3, b3);
+        if (k == 3) break;
+      }
+    }
+    wsync_lds(w);
+  }
+
   // The SOC's costate vector and feed-forward on the stored factorisation:
   //   pc = pv_{k+1} + P_{k+1} c_k,  r = B^T pc + g_u,  k_k = -Q_uu^-1 r,  pv_k = g_x + A^T pc + K^T r.
   // The stage gradients (with the rows' r_soc) are stage-parallel (lane = stage); the recursion runs on
@@ -2223,6 +2360,12 @@ struct WaveSolver {
   MR_SWEEP void soc_backward() {
     MR_UNIFORM_P();
     MR_ASSUME_LDS_STATE();
+#if MR_PHASE_CYCLES
+    unsigned long long tb = trace ? MR_CLOCK() : 0ull;
+#define MR_TSUB(q) do { if (trace) { const unsigned long long tn = MR_CLOCK(); tsub[q] += tn - tb; tb = tn; } } while (0)
+#else
+#define MR_TSUB(q) ((void)0)
+#endif
     const T mu = this->mu, dl = cw()->delta_it;
     const int N = wu(w, this->N);
     if (own()) {
@@ -2258,10 +2401,13 @@ struct WaveSolver {
       for (int i = 0; i < NZ; ++i) Cf(CSF::SG + i) = g[i];
     }
     wsync(w);
+    MR_TSUB(12);
 #if MR_MFMA_SOCB
     // pv_k = Acl_k^T pv_{k+1} + v_k with v_k = A_k^T q + K_k^T u_k + g_x, q = P_{k+1} c_k, u_k = B_k^T q + g_u
-    // (then r_k = B_k^T pv_{k+1} + u_k): v_k, u_k stage-parallel into the cold fields SPV / SK0, the
-    // recursion by mfma_chain<TR>, then r_k and the feed-forward stage-parallel
+    // (then r_k = B_k^T pv_{k+1} + u_k): v_k, u_k stage-parallel into the cold fields SPV / SK0 (everything
+    // that does not depend on pv_{k+1}), then the recursion -- MR_MFMA_SOCB 1: mfma_chain<TR>; 2: a lean
+    // lane recursion (socb_chain: pv_{k+1} broadcast, A_k^T pv + K_k^T (B_k^T pv) + v_k, r_k on the way) --
+    // then the feed-forward stage-parallel
     if (own() && ln < N) {
       const int k = ln;
       const MR_GLOBAL T* Rk = R(k);
@@ -2286,6 +2432,30 @@ struct WaveSolver {
       for (int a = 0; a < NU; ++a) Cf(CSF::SK0 + a) = u[a];
     }
     MR_LDS T* const LDX = lds + LDX_OFF;
+#if MR_MFMA_SOCB == 2
+    wsync(w);  // v_k, u_k (cold fields) visible
+    MR_TSUB(13);
+    socb_chain();
+    MR_TSUB(14);
+    if (own()) {
+      const int k = ln;
+      T pv[NX];
+      for (int r = 0; r < NX; ++r) pv[r] = LDX[k * 12 + r];
+      if (k < N) {
+        const MR_GLOBAL T* Rk = R(k);
+        const T Lf[6] = {T(0), Rk[RCF::LQ + 0], T(0), Rk[RCF::LQ + 1], Rk[RCF::LQ + 2], T(0)};
+        const T iv[3] = {Rk[RCF::LQ + 3], Rk[RCF::LQ + 4], Rk[RCF::LQ + 5]};
+        T kf[NU];
+        for (int a = 0; a < NU; ++a) kf[a] = -lds[LX_OFF + 3 * k + a];  // r_k from the chain
+        lsolve3r(Lf, iv, kf);
+        ltsolve3r(Lf, iv, kf);
+        for (int a = 0; a < NU; ++a) Cf(CSF::SK0 + a) = kf[a];
+      }
+      for (int r = 0; r < NX; ++r) Cf(CSF::SPV + r) = pv[r];
+    }
+    wsync(w);
+    MR_TSUB(15);
+#else
     {  // pv_N = g_x,N: the chain's start (B operand rows 4s + g) and LDX row N
       const int g = ln >> 4;
       const MR_GLOBAL T* cbN = rc + (int64_t)RC_STRIDE * WL + N;
@@ -2319,6 +2489,7 @@ struct WaveSolver {
       for (int r = 0; r < NX; ++r) Cf(CSF::SPV + r) = pv[r];
     }
     wsync(w);
+#endif
 #else
     const MR_GLOBAL T* cb = rc + (int64_t)RC_STRIDE * WL;
     const WBuf<T> wb(rc + (int64_t)RC_STRIDE * WL, (unsigned)CSF::NF * WL);
@@ -2409,6 +2580,7 @@ struct WaveSolver {
     }
     wsync(w);
 #endif
+#undef MR_TSUB
   }
   // the SOC direction (mr_solver.h Solver::forward with soc set): SDZ, SDS, SDLAM, SDY, SDNU.  The recursion
   // is the Newton direction's (fwd_recursion, its lane groups and prefetch) with the SOC's feed-forward,
@@ -3326,6 +3498,10 @@ struct WaveSolver {
       tr[7] = (double)(trace ? MR_CLOCK() - tstart : 0ull);
       double* tr2 = trace + 8 * (trace_cap - 2);  // sub-phases: forward seq/par, eval stage/reduce, failed factorisations (cycles, count), SOC backward / forward
       for (int q = 0; q < 8; ++q) tr2[q] = (double)tsub[q];
+      if (trace_cap >= 3) {  // trial sub-phases: stage values, reductions, acceptance tests; line-search setup
+        double* tr3 = trace + 8 * (trace_cap - 3);
+        for (int q = 0; q < 8; ++q) tr3[q] = (double)tsub[8 + q];
+      }
     }
 #endif
     if (trace && ln == 0 && it < trace_cap - 2) {

@@ -56,6 +56,8 @@ def one(name, b, i, cap=520):
     row = dict(zip(NAMES, tr[-1].tolist()))
     row.update(dict(zip(["fwd_seq", "fwd_par", "socf_chain", "socf_par", "fact_failed_cycles", "n_fact_failed",
                         "soc_backward", "soc_forward"], tr[-2][:8].tolist())))
+    row.update(dict(zip(["trial_stage", "trial_reduce", "trial_accept", "ls_setup", "socb_grad", "socb_pre", "socb_chain",
+                          "socb_post"], tr[-3][:8].tolist())))
     row.update(instance=i, iters=it, status=int(out["status"][0]), wall_ms=1e3 * min(lat),
                cycles_per_iter=row["total"] / max(it, 1))
     return row
@@ -84,6 +86,8 @@ def main():
             row = dict(zip(NAMES, tr[-1].tolist()))
             row.update(dict(zip(["fwd_seq", "fwd_par", "socf_chain", "socf_par", "fact_failed_cycles",
                                  "n_fact_failed", "soc_backward", "soc_forward"], tr[-2][:8].tolist())))
+            row.update(dict(zip(["trial_stage", "trial_reduce", "trial_accept", "ls_setup", "socb_grad", "socb_pre", "socb_chain",
+                          "socb_post"], tr[-3][:8].tolist())))
             row.update(instance=i, iters=it_i, status=int(o["status"][i]), in_batch=True,
                        cycles_per_iter=row["total"] / max(it_i, 1))
             res[name].append(row)
