@@ -76,7 +76,7 @@
 #define MR_MFMA_CHAIN 0  // 1: the forward / SOC recursions as MFMA products of the closed-loop map (A/B option: slower)
 #endif
 #ifndef MR_MFMA_SOCB
-#define MR_MFMA_SOCB 2  // the SOC costate pass on stage-parallel v_k, u_k: 2 the lean lane recursion (socb_chain), 1 the MFMA chain (A/B option), 0 the lane-group recursion
+#define MR_MFMA_SOCB 2  // the SOC costate pass on stage-parallel v_k, u_k: 2 the lane recursion forming A^T pv + K^T B^T pv (socb_chain); A/B options: 3 the lane recursion on a stored closed-loop map (socb_chain_acl: its chain 45 % shorter, the batch 2.3 % slower -- profiles/r05_socb_ab.json), 1 the MFMA chain, 0 the lane-group recursion
 #endif
 #ifndef MR_PRIO_ITER
 #define MR_PRIO_ITER 0  // > 0: the wave raises its issue priority (s_setprio) at this iteration
@@ -152,8 +152,12 @@ struct CSF {
 // the solve precision, [3][NX][64] doubles after the cold fields: eval_sweep forms the stationarity residual and the
 // Riccati right-hand side from them in fp64 (the correction form, see there).
 constexpr int64_t WS_NU_OFF = (int64_t)SSF::NF * WL + (int64_t)RC_STRIDE * WL + (int64_t)CSF::NF * WL;  // words
+// The closed-loop map of the accepted factorisation for the second-order corrections' costate pass
+// (MR_MFMA_SOCB 3): field i NX + j, lane k holds Acl_k[j][i] (Acl = A + B K), after the multipliers.
 template <typename T>
-MR_HD constexpr int64_t ws_words() { return WS_NU_OFF + 3 * NX * WL * (int64_t)(sizeof(double) / sizeof(T)); }
+MR_HD constexpr int64_t ws_mt_off() { return WS_NU_OFF + 3 * NX * WL * (int64_t)(sizeof(double) / sizeof(T)); }
+template <typename T>
+MR_HD constexpr int64_t ws_words() { return ws_mt_off<T>() + (MR_MFMA_SOCB == 3 ? (int64_t)NX * NX * WL : 0); }
 
 // Wave-uniform state of the watchdog and the restoration phase: one copy per wavefront next to the
 // line-search filter (LDS on the device), every lane writing the same values -- not in the per-lane
@@ -323,6 +327,7 @@ struct WaveSolver {
   MR_HD MR_GLOBAL double& NUd(int i) const { return nub()[i * WL + ln]; }
   MR_HD MR_GLOBAL double& WNUd(int i) const { return nub()[(NX + i) * WL + ln]; }
   MR_HD MR_GLOBAL double& ANUd(int i) const { return nub()[(2 * NX + i) * WL + ln]; }  // acceptable-point copy
+  MR_HD MR_GLOBAL T* mtb() const { return rc - (int64_t)SSF::NF * WL + ws_mt_off<T>(); }  // Acl fields
   MR_HD auto& fth(int i) const { return filt[i]; }
   MR_HD auto& fph(int i) const { return filt[FMAX + i]; }
   MR_HD MR_GLOBAL T* R(int k) const { return rc + (int64_t)k * RC_STRIDE; }
@@ -2253,6 +2258,77 @@ struct WaveSolver {
     }
     wsync(w);
   }
+  // The SOC costate recursion on the stored closed-loop map (MR_MFMA_SOCB 3): lane i < NX forms
+  // pv_k[i] = v_k[i] + sum_j Acl_k[j][i] pv_{k+1}[j] -- per stage one broadcast of pv (11 v_readlane) and
+  // an 11-term dot as three chains, its 12 operands (Acl column i, v_k[i]) loaded three stages ahead;
+  // pv_k to LDX row k (LDS only in the loop).  r_k and the feed-forward follow stage-parallel.
+  MR_HD void socb_chain_acl() {
+    const int N = wu(this->w, this->N), ln = this->ln;
+    const Wv w = this->w;
+    const WBuf<T> wb(rc - (int64_t)SSF::NF * WL, (unsigned)WS_NU_OFF);
+    const WBuf<T> mb(mtb(), (unsigned)(NX * NX * WL));
+    const unsigned cold0 = (unsigned)(SSF::NF * WL) + (unsigned)RC_STRIDE * WL;
+    MR_LDS T* const LDX = lds + LDX_OFF;
+    const bool row = ln < NX;
+    const int li = row ? ln : 0;
+    const unsigned voff = (unsigned)(CSF::SPV + li) * WL;
+    unsigned moff[NX];
+#pragma unroll
+    for (int j = 0; j < NX; ++j) moff[j] = (unsigned)(li * NX + j) * WL;
+    // LDS target: row k of LDX for lanes < NX, the lane's discard slot otherwise (address = base + k stride)
+    const int lbase = row ? LDX_OFF + ln : LJUNK_OFF + ln, lstride = row ? 12 : 0;
+    struct Ops {
+      T m[NX], v;
+    };
+    auto ld = [&](int k, Ops& o) {
+      const unsigned ku = (unsigned)wu(w, k), ck = (unsigned)wu(w, (int)(cold0 + (unsigned)k));
+#pragma unroll
+      for (int j = 0; j < NX; ++j) o.m[j] = mb.ld(ku, moff[j]);
+      o.v = wb.ld(ck, voff);
+    };
+    T pv = wb.ld((unsigned)wu(w, (int)(cold0 + (unsigned)N)), (unsigned)(CSF::SG + li) * WL);  // pv_N = g_x,N
+    lds[lbase + lstride * N] = pv;
+    auto step = [&](int k, const Ops& o) {
+      T p[NX];
+      wgather<T, NX>(w, pv, p);
+      T a0 = o.v + o.m[0] * p[0], a1 = o.m[1] * p[1], a2 = o.m[2] * p[2];
+#pragma unroll
+      for (int j = 3; j < NX; j += 3) {
+        a0 += o.m[j] * p[j];
+        if (j + 1 < NX) a1 += o.m[j + 1] * p[j + 1];
+        if (j + 2 < NX) a2 += o.m[j + 2] * p[j + 2];
+      }
+      pv = (a0 + a1) + a2;
+      lds[lbase + lstride * k] = pv;
+    };
+    if (N > 0) {
+      auto kc = [](int k) { return k > 0 ? k : 0; };
+      Ops b0, b1, b2, b3;
+      ld(N - 1, b0);
+      ld(kc(N - 2), b1);
+      ld(kc(N - 3), b2);
+      for (int k = N - 1;; k -= 4) {
+        ld(kc(k - 3), b3);
+        MR_SCHED_BARRIER();
+        step(k, b0);
+        if (k == 0) break;
+        ld(kc(k - 4), b0);
+        MR_SCHED_BARRIER();
+        step(k - 1, b1);
+        if (k == 1) break;
+        ld(kc(k - 5), b1);
+        MR_SCHED_BARRIER();
+        step(k - 2, b2);
+        if (k == 2) break;
+        ld(kc(k - 6), b2);
+        MR_SCHED_BARRIER();
+        step(k - 3, b3);
+        if (k == 3) break;
+      }
+    }
+    wsync_lds(w);
+  }
+
   // The SOC costate recursion given v_k, u_k (cold fields SPV, SK0: everything that does not depend on
   // pv_{k+1}): lane i < NX forms pv_k[i] = v_k[i] + (A_k^T pv_{k+1})[i] + sum_a K_k[a][i] (B_k^T pv_{k+1})[a]
   // from pv_{k+1} broadcast by v_readlane; B_k^T pv_{k+1} (the same in every lane) plus u_k is r_k, the
@@ -2281,20 +2357,20 @@ struct WaveSolver {
       T acol[6], kcol[NU], v, jb[12], u;
     };
     auto ld = [&](int k, Ops& o) {
-      const unsigned rk = (unsigned)wu(w, (int)R(k));
+      const unsigned rk = (unsigned)wu(w, (int)R(k)), ck = (unsigned)wu(w, (int)(cold0 + (unsigned)k));
 #pragma unroll
       for (int j = 0; j < 6; ++j) o.acol[j] = wb.ld(rk, aoff[j]);
 #pragma unroll
       for (int a = 0; a < NU; ++a) o.kcol[a] = wb.ld(rk, koff[a]);
-      o.v = wb.ld(cold0 + (unsigned)k, voff);
+      o.v = wb.ld(ck, voff);
 #pragma unroll
       for (int j = 0; j < 6; ++j) {
         o.jb[2 * j] = wb.ld(rk, (unsigned)(RCF::J + j * 8 + 6));
         o.jb[2 * j + 1] = wb.ld(rk, (unsigned)(RCF::J + j * 8 + 7));
       }
-      o.u = wb.ld(cold0 + (unsigned)k, uoff);  // lane a < NU: u_k[a]
+      o.u = wb.ld(ck, uoff);  // lane a < NU: u_k[a]
     };
-    T pv = wb.ld(cold0 + (unsigned)N, (unsigned)(CSF::SG + li) * WL);  // pv_N = g_x,N
+    T pv = wb.ld((unsigned)wu(w, (int)(cold0 + (unsigned)N)), (unsigned)(CSF::SG + li) * WL);  // pv_N = g_x,N
     LDX[row ? N * 12 + ln : LJUNK_OFF - LDX_OFF + ln] = pv;
     auto step = [&](int k, const Ops& o) {
       T p[NX];
@@ -2326,7 +2402,9 @@ struct WaveSolver {
       lds[ln < NU ? LX_OFF + 3 * k + ln : LJUNK_OFF + ln] = bt + o.u;  // r_k
     };
     // operands three stages ahead, four rotating sets (unrolled by four: no register copies of in-flight
-    // loads); a prefetch past stage 0 re-reads stage 0 (unconditional loads, exact waits)
+    // loads); a prefetch past stage 0 re-reads stage 0 (unconditional loads, exact waits).  Scheduling
+    // barriers keep each prefetch ahead of the step it overlaps (left free, the scheduler sank the loads
+    // to the loop's end, turning the waits into vmcnt(0) drains)
     if (N > 0) {
       auto kc = [](int k) { return k > 0 ? k : 0; };
       Ops b0, b1, b2, b3;
@@ -2335,15 +2413,19 @@ struct WaveSolver {
       ld(kc(N - 3), b2);
       for (int k = N - 1;; k -= 4) {
         ld(kc(k - 3), b3);
+        MR_SCHED_BARRIER();
         step(k, b0);
         if (k == 0) break;
         ld(kc(k - 4), b0);
+        MR_SCHED_BARRIER();
         step(k - 1, b1);
         if (k == 1) break;
         ld(kc(k - 5), b1);
+        MR_SCHED_BARRIER();
         step(k - 2, b2);
         if (k == 2) break;
         ld(kc(k - 6), b2);
+        MR_SCHED_BARRIER();
         step(k - 3, b3);
         if (k == 3) break;
       }
@@ -2420,19 +2502,63 @@ struct WaveSolver {
         q[r] = v;
       }
       for (int j = 0; j < 48; ++j) J[j] = Rk[RCF::J + j];
-      T u[NU], at[NX];
+      T u[NU], at[NX], Kr[NU][NX];
+      for (int a = 0; a < NU; ++a)
+        for (int r = 0; r < NX; ++r) Kr[a][r] = Rk[RCF::K + a * NX + r];
       apply_Bt(J, k, q, u);
       for (int a = 0; a < NU; ++a) u[a] += Cf(CSF::SG + NX + a);
       apply_At(J, k, q, at);
       for (int r = 0; r < NX; ++r) {
         T v = at[r] + Cf(CSF::SG + r);
-        for (int a = 0; a < NU; ++a) v += Rk[RCF::K + a * NX + r] * u[a];
+        for (int a = 0; a < NU; ++a) v += Kr[a][r] * u[a];
         Cf(CSF::SPV + r) = v;
       }
       for (int a = 0; a < NU; ++a) Cf(CSF::SK0 + a) = u[a];
+#if MR_MFMA_SOCB == 3
+      // Acl_k = A_k + B_k K_k (mr_solver.h apply_A / apply_B's structure), column i to fields i NX + j
+      MR_GLOBAL T* const mt = mtb();
+      for (int i = 0; i < NX; ++i) {
+        for (int j = 0; j < 6; ++j) {
+          const T a = i < 6 ? J[j * 8 + i] : T(0);
+          mt[(i * NX + j) * WL + k] = a + J[j * 8 + 6] * Kr[0][i] + J[j * 8 + 7] * Kr[1][i];
+        }
+        mt[(i * NX + 6) * WL + k] = (i == 6 ? T(1) : T(0)) + Kr[2][i];
+        mt[(i * NX + 7) * WL + k] = Kr[0][i];
+        mt[(i * NX + 8) * WL + k] = Kr[1][i];
+        mt[(i * NX + 9) * WL + k] = k > 0 ? (i == 9 ? T(1) : T(0)) : Kr[0][i];
+        mt[(i * NX + 10) * WL + k] = k > 0 ? (i == 10 ? T(1) : T(0)) : Kr[1][i];
+      }
+#endif
     }
     MR_LDS T* const LDX = lds + LDX_OFF;
-#if MR_MFMA_SOCB == 2
+#if MR_MFMA_SOCB == 3
+    wsync(w);  // v_k, u_k (cold fields) and Acl visible
+    MR_TSUB(13);
+    socb_chain_acl();
+    MR_TSUB(14);
+    if (own()) {  // r_k = B_k^T pv_{k+1} + u_k, k_k = -Q_uu^-1 r_k; pv_k to SPV
+      const int k = ln;
+      T pv[NX];
+      for (int r = 0; r < NX; ++r) pv[r] = LDX[k * 12 + r];
+      if (k < N) {
+        const MR_GLOBAL T* Rk = R(k);
+        T pn[NX];
+        for (int r = 0; r < NX; ++r) pn[r] = LDX[(k + 1) * 12 + r];
+        T r0 = pn[7], r1 = pn[8];
+        if (k == 0) { r0 += pn[9]; r1 += pn[10]; }
+        for (int j = 0; j < 6; ++j) { r0 += Rk[RCF::J + j * 8 + 6] * pn[j]; r1 += Rk[RCF::J + j * 8 + 7] * pn[j]; }
+        const T Lf[6] = {T(0), Rk[RCF::LQ + 0], T(0), Rk[RCF::LQ + 1], Rk[RCF::LQ + 2], T(0)};
+        const T iv[3] = {Rk[RCF::LQ + 3], Rk[RCF::LQ + 4], Rk[RCF::LQ + 5]};
+        T kf[NU] = {-(r0 + Cf(CSF::SK0 + 0)), -(r1 + Cf(CSF::SK0 + 1)), -(pn[6] + Cf(CSF::SK0 + 2))};
+        lsolve3r(Lf, iv, kf);
+        ltsolve3r(Lf, iv, kf);
+        for (int a = 0; a < NU; ++a) Cf(CSF::SK0 + a) = kf[a];
+      }
+      for (int r = 0; r < NX; ++r) Cf(CSF::SPV + r) = pv[r];
+    }
+    wsync(w);
+    MR_TSUB(15);
+#elif MR_MFMA_SOCB == 2
     wsync(w);  // v_k, u_k (cold fields) visible
     MR_TSUB(13);
     socb_chain();
