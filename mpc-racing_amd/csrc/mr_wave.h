@@ -78,6 +78,9 @@
 #ifndef MR_MFMA_SOCB
 #define MR_MFMA_SOCB 2  // the SOC costate pass on stage-parallel v_k, u_k: 2 the lane recursion forming A^T pv + K^T B^T pv (socb_chain); A/B options: 3 the lane recursion on a stored closed-loop map (socb_chain_acl: its chain 45 % shorter, the batch 2.3 % slower -- profiles/r05_socb_ab.json), 1 the MFMA chain, 0 the lane-group recursion
 #endif
+#ifndef MR_SOC_CAPTURE
+#define MR_SOC_CAPTURE 1  // a SOC trial point's constraint values captured by its evaluation (LS_CAP), not re-evaluated
+#endif
 #ifndef MR_PRIO_ITER
 #define MR_PRIO_ITER 0  // > 0: the wave raises its issue priority (s_setprio) at this iteration
 #endif
@@ -141,7 +144,10 @@ struct CSF {
     RDVN = RDVP + NI, RY = RDVN + NI, RDY = RY + NI, RZ = RDY + NI,
     CP = RZ + NZS, CN = CP + 6, CVP = CN + 6, CVN = CVP + 6, CDP = CVN + 6, CDN = CDP + 6, CDVP = CDN + 6,
     CDVN = CDVP + 6, CSW = CDVN + 6, CGW0 = CSW + 6, CGW1 = CGW0 + 6,
-    SJUNK = CGW1 + 6,  // discard slot of the SOC chains' lanes without a component
+    // a trial point's constraint values captured for the second-order correction that may follow it
+    // (LS_CAP): the rows' (d - s) (NI) and the dynamics defects (NX), 0 where none is accumulated
+    CTR = CGW1 + 6, CTC = CTR + NI,
+    SJUNK = CTC + NX,  // discard slot of the SOC chains' lanes without a component
     // the filter's entries beyond the FMAX in LDS (mr_solver.h FCAP): [bank][theta | phi][FOVF] fields, entry
     // FMAX + 64 q + l in lane l of field q; bank 0 the original problem's, bank 1 the restoration phase's
     FOV = SJUNK + 1,
@@ -1970,11 +1976,14 @@ struct WaveSolver {
   //   LS_FORCE  one trial, stored whatever its acceptance;
   //   LS_ACC    one trial, accumulate its constraint values into the SOC right-hand sides
   //             (SC = acc SC + c(trial), SR = acc SR + (d - s)(trial)), nothing stored;
+  //   LS_CAP    the first trial's constraint values are also written to the cold fields CTR / CTC, so a
+  //             second-order correction of that trial point accumulates them (soc_accumulate) instead of
+  //             evaluating the point again;
   //   otherwise backtracking; a rejected first trial (a0 = the fraction-to-boundary step, theta not
   //   decreased) returns with LS_NEED_SOC so the caller runs the second-order corrections.
   // SOCDIR: the trial points lie along the SOC direction (SDZ, SDS) instead of the Newton direction.
   // RESTO: the restoration phase's NLP (mr_solver.h trial() with resto set).
-  enum { LS_WD = 1, LS_FORCE = 2, LS_ACC = 4, LS_NOSOC = 8 };
+  enum { LS_WD = 1, LS_FORCE = 2, LS_ACC = 4, LS_NOSOC = 8, LS_CAP = 16 };
   enum { LSR_ACC = 1, LSR_AUG = 2, LSR_REJF = 4, LSR_NEED_SOC = 8, LSR_FIN = 16 };
   template <bool RESTO, bool SOCDIR>
   MR_SWEEP void line_search(T th, T ph, T gphi, T th_pow, T a0, T a_max, T a_min, int nls0, int mode, T a_fix,
@@ -2046,7 +2055,7 @@ struct WaveSolver {
     const T kdm = T(IP_KAPPA_D) * mu;
     // one trial point: zt, st (registers), theta, phi; false if a slack is not positive or a value is
     // not finite.  accum: add its constraint values to the SOC right-hand sides (SC, SR)
-    auto eval = [&](T alpha, bool accum, T& th_t, T& ph_t) -> bool {
+    auto eval = [&](T alpha, bool accum, T& th_t, T& ph_t, bool cap) -> bool {
 #if MR_PHASE_CYCLES
       const unsigned long long te0 = trace ? MR_CLOCK() : 0ull;
 #endif
@@ -2066,7 +2075,10 @@ struct WaveSolver {
         row_values(k, zt, e, d, act);
         for (int j = 0; j < NI; ++j) {
           st[j] = s_c[j];
-          if (!((actm >> j) & 1u)) continue;
+          if (!((actm >> j) & 1u)) {
+            if (!RESTO && cap) Cf(CSF::CTR + j) = T(0);
+            continue;
+          }
           const T sj = s_c[j] + alpha * ds[j];
           if (!(sj > T(0))) ok_l = 0;
           st[j] = sj;
@@ -2082,6 +2094,9 @@ struct WaveSolver {
           } else if (yslot(j)) {
             th_l += mr_abs(d[j] - sj);
             if (accum) Cf(CSF::SR + j) = acc * Cf(CSF::SR + j) + T(slot_sign(j)) * (d[j] - sj);
+            if (cap) Cf(CSF::CTR + j) = T(slot_sign(j)) * (d[j] - sj);
+          } else if (cap) {
+            Cf(CSF::CTR + j) = T(0);
           }
         }
         if constexpr (RESTO) {
@@ -2110,8 +2125,11 @@ struct WaveSolver {
             for (int i = 0; i < NX; ++i) {
               th_l += mr_abs(xn[i] - ztn[i]);
               if (accum) Cf(CSF::SC + i) = acc * Cf(CSF::SC + i) + (xn[i] - ztn[i]);
+              if (cap) Cf(CSF::CTC + i) = xn[i] - ztn[i];
             }
           }
+        } else if (!RESTO && cap) {
+          for (int i = 0; i < NX; ++i) Cf(CSF::CTC + i) = T(0);
         }
       }
 #if MR_PHASE_CYCLES
@@ -2142,7 +2160,7 @@ struct WaveSolver {
     bool store = false;
     if (mode & (LS_FORCE | LS_ACC)) {
       alpha = a_fix;
-      const bool fin = eval(alpha, (mode & LS_ACC) != 0, th_t, ph_t);
+      const bool fin = eval(alpha, (mode & LS_ACC) != 0, th_t, ph_t, false);
       ntr++;
       flags |= fin ? LSR_FIN : 0;
       store = (mode & LS_FORCE) != 0;
@@ -2151,7 +2169,7 @@ struct WaveSolver {
       for (int n = 0; n < IP_LS_MAX; ++n) {
         if (!(alpha > a_min || n == 0)) break;
         a_test = (mode & LS_WD) ? a_fix : alpha;
-        const bool fin = eval(alpha, false, th_t, ph_t);
+        const bool fin = eval(alpha, false, th_t, ph_t, !RESTO && (mode & LS_CAP) && n == 0);
         ntr++;
 #if MR_PHASE_CYCLES
         const unsigned long long ta0 = trace ? MR_CLOCK() : 0ull;
@@ -2255,6 +2273,16 @@ struct WaveSolver {
       row_values(k, z, e, d, act);
       for (int j = 0; j < NI; ++j)
         Cf(CSF::SR + j) = (act[j] && yslot(j)) ? T(slot_sign(j)) * (d[j] - S(sf(cur) + j)) : T(0);
+    }
+    wsync(w);
+  }
+  // SC = acc SC + c(trial), SR = acc SR + (d - s)(trial) from the values the trial's evaluation captured
+  // (LS_CAP; 0 where LS_ACC's evaluation accumulates nothing, so the fields it leaves alone stay 0)
+  MR_SWEEP void soc_accumulate(T acc) {
+    MR_ASSUME_LDS_STATE();
+    if (own()) {
+      for (int j = 0; j < NI; ++j) Cf(CSF::SR + j) = acc * Cf(CSF::SR + j) + Cf(CSF::CTR + j);
+      for (int i = 0; i < NX; ++i) Cf(CSF::SC + i) = acc * Cf(CSF::SC + i) + Cf(CSF::CTC + i);
     }
     wsync(w);
   }
@@ -3480,7 +3508,7 @@ struct WaveSolver {
             accepted = (flags & LSR_ACC) != 0;
           }
         } else {
-          line_search<false, false>(th, ph, gphi, th_pow, ap, ap, a_min, 0, 0, T(0), T(-1));
+          line_search<false, false>(th, ph, gphi, th_pow, ap, ap, a_min, 0, MR_SOC_CAPTURE ? LS_CAP : 0, T(0), T(-1));
           flags = res_flags;
           rejf |= (flags & LSR_REJF) != 0;
           accepted = (flags & LSR_ACC) != 0;
@@ -3493,7 +3521,11 @@ struct WaveSolver {
             for (int count = 0; count < IP_MAX_SOC; ++count) {
               if (count > 0 && !(th_trial <= T(IP_KAPPA_SOC) * th_old)) break;
               th_old = th_trial;
-              if (count == 0)
+              // the trial point's constraint values: captured by its own evaluation (the first trial of the
+              // line search, or the previous correction's trial), else evaluated again
+              if (MR_SOC_CAPTURE)
+                soc_accumulate(a_soc);
+              else if (count == 0)
                 line_search<false, false>(th, ph, gphi, th_pow, a_soc, ap, a_min, 0, LS_ACC, a_soc, a_soc);
               else
                 line_search<false, true>(th, ph, gphi, th_pow, a_soc, ap, a_min, 0, LS_ACC, a_soc, a_soc);
@@ -3511,7 +3543,8 @@ struct WaveSolver {
 #if MR_PHASE_CYCLES
               if (trace) { tsub[6] += ts1 - ts0; tsub[7] += MR_CLOCK() - ts1; }
 #endif
-              line_search<false, true>(th, ph, gphi, th_pow, aps, aps, aps, 0, LS_WD, a_test0, T(-1));
+              line_search<false, true>(th, ph, gphi, th_pow, aps, aps, aps, 0, MR_SOC_CAPTURE ? (LS_WD | LS_CAP) : LS_WD,
+                                       a_test0, T(-1));
               rejf |= (res_flags & LSR_REJF) != 0;
               a_soc = aps;
               if (!(res_flags & LSR_FIN)) break;
