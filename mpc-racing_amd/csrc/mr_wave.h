@@ -21,6 +21,7 @@
 //   nu[2][11][64] the dynamics rows' multipliers and their watchdog copy, fp64 in both precisions
 #pragma once
 #include <new>
+#include <type_traits>
 
 #include "mr_batch.h"
 #include "mr_wave_prims.h"
@@ -77,6 +78,12 @@
 #endif
 #ifndef MR_MFMA_SOCB
 #define MR_MFMA_SOCB 2  // the SOC costate pass on stage-parallel v_k, u_k: 2 the lane recursion forming A^T pv + K^T B^T pv (socb_chain); A/B options: 3 the lane recursion on a stored closed-loop map (socb_chain_acl: its chain 45 % shorter, the batch 2.3 % slower -- profiles/r05_socb_ab.json), 1 the MFMA chain, 0 the lane-group recursion
+#endif
+#ifndef MR_FWD_UNROLL6
+#define MR_FWD_UNROLL6 0  // 1: the forward recursion unrolled by six (A/B option)
+#endif
+#ifndef MR_SOC_GPRE
+#define MR_SOC_GPRE 0  // 1: the SOC costate pass's fixed gradient terms stored once per SOC episode (A/B option: 93.5 vs 92.5 ms, profiles/r05_riccati_pick_ab.json)
 #endif
 #ifndef MR_SOC_CAPTURE
 #define MR_SOC_CAPTURE 1  // a SOC trial point's constraint values captured by its evaluation (LS_CAP), not re-evaluated
@@ -147,7 +154,11 @@ struct CSF {
     // a trial point's constraint values captured for the second-order correction that may follow it
     // (LS_CAP): the rows' (d - s) (NI) and the dynamics defects (NX), 0 where none is accumulated
     CTR = CGW1 + 6, CTC = CTR + NI,
-    SJUNK = CTC + NX,  // discard slot of the SOC chains' lanes without a component
+    // the SOC costate pass's gradient terms that stay fixed over an SOC episode (soc_prepare): the base
+    // G0 + mu G1 + delta GD, per row (c0, c1, e0, e1) with dg = c0 (SR0 - e0) + c1 (SR1 + e1), the lane
+    // row's e_C gradient
+    SGB = CTC + NX, SGR = SGB + NZ, SGC = SGR + 4 * (NROW + 1),
+    SJUNK = SGC + 3,  // discard slot of the SOC chains' lanes without a component
     // the filter's entries beyond the FMAX in LDS (mr_solver.h FCAP): [bank][theta | phi][FOVF] fields, entry
     // FMAX + 64 q + l in lane l of field q; bank 0 the original problem's, bank 1 the restoration phase's
     FOV = SJUNK + 1,
@@ -257,6 +268,16 @@ MR_HD bool chol3r(const T* R, T* L, T* iv) {
   iv[2] = mr_rsqrt(ok2 ? d2 : T(1));
   L[0] = T(0); L[1] = l10; L[2] = T(0); L[3] = l20; L[4] = l21; L[5] = T(0);
   return ok0 & ok1 & ok2;
+}
+// a_l for lane l (l >= 5: a5) by lane-constant bit masks -- no branches, exact for any bit pattern
+template <typename T>
+MR_HD T pick6(int l, T a0, T a1, T a2, T a3, T a4, T a5) {
+  typedef typename std::conditional<sizeof(T) == 4, unsigned, unsigned long long>::type U;
+  const U z = U(0), o = ~U(0);
+  const U r = (__builtin_bit_cast(U, a0) & (l == 0 ? o : z)) | (__builtin_bit_cast(U, a1) & (l == 1 ? o : z)) |
+              (__builtin_bit_cast(U, a2) & (l == 2 ? o : z)) | (__builtin_bit_cast(U, a3) & (l == 3 ? o : z)) |
+              (__builtin_bit_cast(U, a4) & (l == 4 ? o : z)) | (__builtin_bit_cast(U, a5) & (l >= 5 ? o : z));
+  return __builtin_bit_cast(T, r);
 }
 template <typename T>
 MR_HD void lsolve3r(const T* L, const T* iv, T* b) {
@@ -1274,7 +1295,9 @@ struct WaveSolver {
       T L[6], iv[3];
       const bool piv_ok = chol3r(Rh, L, iv);  // checked every second stage (below)
       {  // Q_uu's factor for second-order corrections: lanes 0..5 store L10, L20, L21, 1/L00, 1/L11, 1/L22
-        const T lq = l == 0 ? L[1] : (l == 1 ? L[3] : (l == 2 ? L[4] : (l == 3 ? iv[0] : (l == 4 ? iv[1] : iv[2]))));
+        // selected by lane-constant bit masks: the nested conditional compiled to a divergent branch tree
+        // (~40 scalar and exec-mask instructions per stage)
+        const T lq = pick6(l, L[1], L[3], L[4], iv[0], iv[1], iv[2]);
         rb.st(lq, Rk, l < 6 ? (unsigned)(RCF::LQ + l) : (unsigned)RCF::JUNK);
       }
       T w0[3] = {qat(11, 14), qat(12, 14), qat(13, 14)};
@@ -1443,6 +1466,30 @@ struct WaveSolver {
       FwdRow fa, fb, fc;
       fload(0, fa);
       fload(1, fb);
+#if MR_FWD_UNROLL6
+      // unrolled by six over the three sets: the compiler's wait at the loop head (its merge of the
+      // back-edge state is conservative, vmcnt drains the older set too) hits one step in six, not three
+      for (int k = 0;; k += 6) {
+        fload(k + 2, fc);
+        fstep(k, fa);
+        if (k == N) break;
+        fload(k + 3, fa);
+        fstep(k + 1, fb);
+        if (k + 1 == N) break;
+        fload(k + 4, fb);
+        fstep(k + 2, fc);
+        if (k + 2 == N) break;
+        fload(k + 5, fc);
+        fstep(k + 3, fa);
+        if (k + 3 == N) break;
+        fload(k + 6, fa);
+        fstep(k + 4, fb);
+        if (k + 4 == N) break;
+        fload(k + 7, fb);
+        fstep(k + 5, fc);
+        if (k + 5 == N) break;
+      }
+#else
       for (int k = 0;; k += 3) {
         fload(k + 2, fc);
         fstep(k, fa);
@@ -1454,6 +1501,7 @@ struct WaveSolver {
         fstep(k + 2, fc);
         if (k + 2 == N) break;
       }
+#endif
       wsync_lds(w);
       if (ln <= N)
         for (int j = 0; j < NX; ++j) dz[j] = LDX[ln * 12 + j];
@@ -2273,6 +2321,27 @@ struct WaveSolver {
       row_values(k, z, e, d, act);
       for (int j = 0; j < NI; ++j)
         Cf(CSF::SR + j) = (act[j] && yslot(j)) ? T(slot_sign(j)) * (d[j] - S(sf(cur) + j)) : T(0);
+#if MR_SOC_GPRE
+      // the costate pass's fixed gradient terms (soc_backward: only SR changes between the tries)
+      const T mu = this->mu, dl = cw()->delta_it;
+      const MR_GLOBAL T* Rk = R(k);
+      for (int i = 0; i < NZ; ++i) Cf(CSF::SGB + i) = Rk[RCF::G0 + i] + mu * Rk[RCF::G1 + i] + dl * Rk[RCF::GD + i];
+#pragma unroll
+      for (int r = 0; r <= NROW; ++r) {
+        const int j0 = r < NROW ? 2 * r : JL, j1 = j0 + 1;
+        T c0 = T(0), c1 = T(0), e0 = T(0), e1 = T(0);
+        if (act[j0]) {
+          const T t0 = S(sf(cur) + j0), t1 = S(sf(cur) + j1);
+          const T s0 = S(SSF::LAM + j0) / t0, s1 = S(SSF::LAM + j1) / t1;
+          e0 = d[j0] - t0;
+          if (r < 2) { c0 = s0 + dl; c1 = s1 + dl; e1 = d[j1] - t1; }
+          else c0 = s0 + s1 + dl;
+        }
+        Cf(CSF::SGR + 4 * r) = c0; Cf(CSF::SGR + 4 * r + 1) = c1;
+        Cf(CSF::SGR + 4 * r + 2) = e0; Cf(CSF::SGR + 4 * r + 3) = e1;
+      }
+      for (int a = 0; a < 3; ++a) Cf(CSF::SGC + a) = e.gC[a];
+#endif
     }
     wsync(w);
   }
@@ -2400,6 +2469,10 @@ struct WaveSolver {
     };
     T pv = wb.ld((unsigned)wu(w, (int)(cold0 + (unsigned)N)), (unsigned)(CSF::SG + li) * WL);  // pv_N = g_x,N
     LDX[row ? N * 12 + ln : LJUNK_OFF - LDX_OFF + ln] = pv;
+    // the LDS base in a register (a member read after an LDS store is reloaded from the solver object,
+    // itself in LDS: one LDS round trip per step); r_k's slot (lanes < NU) or the lane's discard slot
+    MR_LDS T* const LB = lds;
+    const int rbase = ln < NU ? LX_OFF + ln : LJUNK_OFF + ln, rstride = ln < NU ? 3 : 0;
     auto step = [&](int k, const Ops& o) {
       T p[NX];
       wgather<T, NX>(w, pv, p);
@@ -2427,7 +2500,7 @@ struct WaveSolver {
       pv = o.v + at + o.kcol[0] * b0 + o.kcol[1] * b1 + o.kcol[2] * b2;
       LDX[row ? k * 12 + ln : LJUNK_OFF - LDX_OFF + ln] = pv;
       const T bt = lr == 0 ? b0 : (lr == 1 ? b1 : b2);
-      lds[ln < NU ? LX_OFF + 3 * k + ln : LJUNK_OFF + ln] = bt + o.u;  // r_k
+      LB[rbase + rstride * k] = bt + o.u;  // r_k
     };
     // operands three stages ahead, four rotating sets (unrolled by four: no register copies of in-flight
     // loads); a prefetch past stage 0 re-reads stage 0 (unconditional loads, exact waits).  Scheduling
@@ -2478,6 +2551,32 @@ struct WaveSolver {
 #endif
     const T mu = this->mu, dl = cw()->delta_it;
     const int N = wu(w, this->N);
+#if MR_SOC_GPRE
+    (void)mu; (void)dl;
+    if (own()) {  // g from soc_prepare's fixed terms and this try's SR (same arithmetic as below)
+      T g[NZ];
+      for (int i = 0; i < NZ; ++i) g[i] = Cf(CSF::SGB + i);
+#pragma unroll
+      for (int r = 0; r <= NROW; ++r) {
+        const int j0 = r < NROW ? 2 * r : JL, j1 = j0 + 1;
+        const T c0 = Cf(CSF::SGR + 4 * r), c1 = Cf(CSF::SGR + 4 * r + 1);
+        const T e0 = Cf(CSF::SGR + 4 * r + 2), e1 = Cf(CSF::SGR + 4 * r + 3);
+        if (c0 == T(0) && c1 == T(0)) continue;  // inactive row (an active row's c0 = lam / s + delta > 0)
+        T dg;
+        if (r < 2) dg = c0 * (Cf(CSF::SR + j0) - e0) + c1 * (Cf(CSF::SR + j1) + e1);
+        else dg = c0 * (Cf(CSF::SR + j0) - e0);
+        if (r < NROW) {
+#pragma unroll
+          for (int a = 0; a < RN(r); ++a) g[RI(r, a)] += T(RS(a)) * dg;
+        } else {
+          g[0] += Cf(CSF::SGC + 0) * dg;
+          g[1] += Cf(CSF::SGC + 1) * dg;
+          g[6] += Cf(CSF::SGC + 2) * dg;
+        }
+      }
+      for (int i = 0; i < NZ; ++i) Cf(CSF::SG + i) = g[i];
+    }
+#else
     if (own()) {
       const int k = ln;
       const MR_GLOBAL T* Rk = R(k);
@@ -2510,6 +2609,7 @@ struct WaveSolver {
       }
       for (int i = 0; i < NZ; ++i) Cf(CSF::SG + i) = g[i];
     }
+#endif
     wsync(w);
     MR_TSUB(12);
 #if MR_MFMA_SOCB
