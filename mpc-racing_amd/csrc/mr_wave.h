@@ -82,6 +82,9 @@
 #ifndef MR_FWD_UNROLL6
 #define MR_FWD_UNROLL6 0  // 1: the forward recursion unrolled by six (A/B option)
 #endif
+#ifndef MR_LS_BRANCHFREE
+#define MR_LS_BRANCHFREE 1  // the trial evaluation's slot loop without per-slot branches
+#endif
 #ifndef MR_SOC_GPRE
 #define MR_SOC_GPRE 0  // 1: the SOC costate pass's fixed gradient terms stored once per SOC episode (A/B option: 93.5 vs 92.5 ms, profiles/r05_riccati_pick_ab.json)
 #endif
@@ -2121,7 +2124,32 @@ struct WaveSolver {
         T d[NI];
         int act[NI];
         row_values(k, zt, e, d, act);
+#if MR_LS_BRANCHFREE
+        if constexpr (!RESTO) {
+          // branch-free over the slots (the per-slot activity test compiled to a divergent branch each):
+          // an inactive slot has s = 1, ds = 0 (setup above), so s + alpha ds = 1 > 0 and log 1 = 0 add
+          // nothing, and its other terms are selected out -- the same sums as the branching form
+#pragma unroll
+          for (int j = 0; j < NI; ++j) {
+            const bool a = (actm >> j) & 1u;
+            const T sj = s_c[j] + alpha * ds[j];
+            ok_l &= sj > T(0) ? 1 : 0;
+            st[j] = sj;
+            lg_l += mr_log(sj > T(0) ? sj : T(1));
+            if (oneslot(j)) lin_l += a ? sj : T(0);
+            if (yslot(j)) {
+              const T r = d[j] - sj;
+              th_l += a ? mr_abs(r) : T(0);
+              if (accum && a) Cf(CSF::SR + j) = acc * Cf(CSF::SR + j) + T(slot_sign(j)) * r;
+              if (cap) Cf(CSF::CTR + j) = a ? T(slot_sign(j)) * r : T(0);
+            } else if (cap) {
+              Cf(CSF::CTR + j) = T(0);
+            }
+          }
+        }
+#endif
         for (int j = 0; j < NI; ++j) {
+          if (MR_LS_BRANCHFREE && !RESTO) break;
           st[j] = s_c[j];
           if (!((actm >> j) & 1u)) {
             if (!RESTO && cap) Cf(CSF::CTR + j) = T(0);
