@@ -82,6 +82,9 @@
 #ifndef MR_FWD_UNROLL6
 #define MR_FWD_UNROLL6 0  // 1: the forward recursion unrolled by six (A/B option)
 #endif
+#ifndef MR_EVAL_BRANCHFREE
+#define MR_EVAL_BRANCHFREE 0  // 1: the evaluation sweep's slot loop and row_steps branch-free (A/B option: 96.2 vs 91.5 ms -- every slot's fields loaded and stored, profiles/r05_eval_branchfree_ab.json)
+#endif
 #ifndef MR_LS_BRANCHFREE
 #define MR_LS_BRANCHFREE 1  // the trial evaluation's slot loop without per-slot branches
 #endif
@@ -780,7 +783,48 @@ struct WaveSolver {
       row_values(k, z, e, d, act);
       T lam_j[NI], s_j[NI];
       T sg_j[NI], c0_j[NI], c1_j[NI], y_j[NI];  // restoration: condensed row data (row_cond_r), multipliers y
+#if MR_EVAL_BRANCHFREE
+      if constexpr (!RESTO) {
+        // branch-free over the slots: an inactive slot's operands are replaced (s = 1), its terms selected
+        // out and its multipliers written back unchanged -- the same sums and fields as the branching form
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const bool a = act[j] != 0;
+          sg_j[j] = c0_j[j] = c1_j[j] = T(0);
+          const T sv = S(sf(cur) + j), lv = S(SSF::LAM + j), dlv = S(SSF::DLAM + j);
+          const T s = a ? sv : T(1);
+          T lam = lv + alpha_d * dlv;
+          lam = mr_min(mr_max(lam, mu_prev / (kappa_sigma * s)), kappa_sigma * mu_prev / s);
+          lam = a ? lam : lv;
+          S(SSF::LAM + j) = lam;
+          lam_j[j] = a ? lam : T(0);
+          s_j[j] = s;
+          const T rd = d[j] - s;
+          const T sl = s * lam;
+          smax_l = a ? mr_max(smax_l, sl) : smax_l;
+          smin_l = a ? mr_min(smin_l, sl) : smin_l;
+          lam1_l += a ? mr_abs(lam) : T(0);
+          lg_l += a ? mr_log(s) : T(0);
+          mi_l += a ? 1 : 0;
+          viol_l = a ? mr_max(viol_l, -d[j]) : viol_l;
+          if (oneslot(j)) lin_l += a ? s : T(0);
+          y_j[j] = T(0);
+          if (yslot(j)) {
+            pro_l = a ? mr_max(pro_l, mr_abs(rd)) : pro_l;
+            const T yv = S(SSF::Y + j);
+            const T y = a ? yv + alpha_p * S(SSF::DY + j) : yv;
+            S(SSF::Y + j) = y;
+            y_j[j] = a ? y : T(0);
+            y1_l += a ? mr_abs(y) : T(0);
+            mrow_l += a ? 1 : 0;
+            pr_l = a ? mr_max(pr_l, mr_abs(rd)) : pr_l;
+            th_l += a ? mr_abs(rd) : T(0);
+          }
+        }
+      }
+#endif
       for (int j = 0; j < NI; ++j) {
+        if (MR_EVAL_BRANCHFREE && !RESTO) break;
         lam_j[j] = T(0);
         s_j[j] = T(1);
         sg_j[j] = c0_j[j] = c1_j[j] = y_j[j] = T(0);
@@ -1845,9 +1889,18 @@ struct WaveSolver {
 #pragma unroll
     for (int r = 0; r <= NROW; ++r) {
       const int j0 = r < NROW ? 2 * r : JL, j1 = j0 + 1;
+#if MR_EVAL_BRANCHFREE
+      // branch-free: an inactive row's operands are replaced by s = lam = 1 and its results selected out
+      // (its step fields written 0; every reader masks them by the row's activity)
+      const bool a = act[j0] != 0;
+      const T t0 = a ? S(sf(cur) + j0) : T(1), t1 = a ? S(sf(cur) + j1) : T(1);
+      const T l0 = a ? S(SSF::LAM + j0) : T(1), l1 = a ? S(SSF::LAM + j1) : T(1);
+#else
       if (!act[j0]) continue;
+      const bool a = true;
       const T t0 = S(sf(cur) + j0), t1 = S(sf(cur) + j1);
       const T l0 = S(SSF::LAM + j0), l1 = S(SSF::LAM + j1);
+#endif
       const T s0 = l0 / t0, s1 = l1 / t1;
       T dt0, dt1, dy0, dy1;
       if (r < 2) {
@@ -1858,7 +1911,7 @@ struct WaveSolver {
         dt1 = -Ds1;
         dy0 = (s0 + dl) * Ds0 - mu / t0 + kd * mu - S(SSF::Y + j0);
         dy1 = (s1 + dl) * Ds1 + mu / t1 - kd * mu - S(SSF::Y + j1);
-        if (!SOC) g_l += kd * mu * (dt0 + dt1);
+        if (!SOC) g_l += a ? kd * mu * (dt0 + dt1) : T(0);
       } else {
         const T R0 = SOC ? Cf(CSF::SR + j0) : d[j0] - t0;
         const T Ds = adz[j0] + R0;
@@ -1867,7 +1920,8 @@ struct WaveSolver {
         dy0 = (s0 + s1 + dl) * Ds - mu / t0 + mu / t1 - S(SSF::Y + j0);
         dy1 = T(0);
       }
-      const T dv0 = mu / t0 - l0 - s0 * dt0, dv1 = mu / t1 - l1 - s1 * dt1;
+      T dv0 = mu / t0 - l0 - s0 * dt0, dv1 = mu / t1 - l1 - s1 * dt1;
+      if (!a) { dt0 = dt1 = dv0 = dv1 = dy0 = dy1 = T(0); }
       if constexpr (SOC) {
         Cf(CSF::SDS + j0) = dt0; Cf(CSF::SDS + j1) = dt1;
         Cf(CSF::SDLAM + j0) = dv0; Cf(CSF::SDLAM + j1) = dv1;
@@ -1878,10 +1932,10 @@ struct WaveSolver {
         S(SSF::DY + j0) = dy0; S(SSF::DY + j1) = dy1;
         g_l -= mu * dt0 / t0 + mu * dt1 / t1;
       }
-      if (dt0 < T(0)) ap_l = mr_min(ap_l, -tau * t0 / dt0);
-      if (dt1 < T(0)) ap_l = mr_min(ap_l, -tau * t1 / dt1);
-      if (dv0 < T(0)) ad_l = mr_min(ad_l, -tau * l0 / dv0);
-      if (dv1 < T(0)) ad_l = mr_min(ad_l, -tau * l1 / dv1);
+      ap_l = dt0 < T(0) ? mr_min(ap_l, -tau * t0 / dt0) : ap_l;
+      ap_l = dt1 < T(0) ? mr_min(ap_l, -tau * t1 / dt1) : ap_l;
+      ad_l = dv0 < T(0) ? mr_min(ad_l, -tau * l0 / dv0) : ad_l;
+      ad_l = dv1 < T(0) ? mr_min(ad_l, -tau * l1 / dv1) : ad_l;
     }
   }
 
