@@ -2584,33 +2584,30 @@ struct WaveSolver {
       const T bt = lr == 0 ? b0 : (lr == 1 ? b1 : b2);
       LB[rbase + rstride * k] = bt + o.u;  // r_k
     };
-    // operands three stages ahead, four rotating sets (unrolled by four: no register copies of in-flight
-    // loads); a prefetch past stage 0 re-reads stage 0 (unconditional loads, exact waits).  Scheduling
-    // barriers keep each prefetch ahead of the step it overlaps (left free, the scheduler sank the loads
-    // to the loop's end, turning the waits into vmcnt(0) drains)
+    // operands two stages ahead, three rotating sets (unrolled by three: no register copies of in-flight
+    // loads); a prefetch past stage 0 re-reads stage 0 (unconditional loads, exact waits).  Two ahead, not
+    // three: a wave has at most 63 vector-memory instructions outstanding (vmcnt), and 17 loads per stage
+    // x 4 sets exceeded it, stalling every prefetch's issue on the oldest load (tools/ubench/
+    // chain_loads_ubench.hip: 17 loads x 4 sets 969 cycles per stage, 11 x 4 271).  Scheduling barriers keep
+    // each prefetch ahead of the step it overlaps (left free, the scheduler sank the loads to the loop's end)
     if (N > 0) {
       auto kc = [](int k) { return k > 0 ? k : 0; };
-      Ops b0, b1, b2, b3;
+      Ops b0, b1, b2;
       ld(N - 1, b0);
       ld(kc(N - 2), b1);
-      ld(kc(N - 3), b2);
-      for (int k = N - 1;; k -= 4) {
-        ld(kc(k - 3), b3);
+      for (int k = N - 1;; k -= 3) {
+        ld(kc(k - 2), b2);
         MR_SCHED_BARRIER();
         step(k, b0);
         if (k == 0) break;
-        ld(kc(k - 4), b0);
+        ld(kc(k - 3), b0);
         MR_SCHED_BARRIER();
         step(k - 1, b1);
         if (k == 1) break;
-        ld(kc(k - 5), b1);
+        ld(kc(k - 4), b1);
         MR_SCHED_BARRIER();
         step(k - 2, b2);
         if (k == 2) break;
-        ld(kc(k - 6), b2);
-        MR_SCHED_BARRIER();
-        step(k - 3, b3);
-        if (k == 3) break;
       }
     }
     wsync_lds(w);
