@@ -2284,6 +2284,16 @@ struct WaveSolver {
     if (trace) tsub[11] += MR_CLOCK() - tls0;
 #endif
     const LSRef<T> ref{th, ph, gphi, th_pow};
+    // the reference point's transcendental terms, once per line search (is_ftype's (-gphi)^2.3 and
+    // acc_to_iterate's log10 |phi|; the same expressions, so the same values, as the per-trial forms)
+    const T gpow = gphi < T(0) ? mr_exp(T(2.3) * mr_log(-gphi)) : T(0);
+    const T phbas = mr_abs(ph) > T(10) ? mr_log(mr_abs(ph)) / mr_log(T(10)) : T(1);
+    auto ftype = [&](T at) { return gphi < T(0) && at * gpow > th_pow; };
+    auto acc_it = [&](T tht, T pht) {
+      if (pht > ph && mr_log(pht - ph) / mr_log(T(10)) > T(IP_OBJ_MAX_INC) + phbas) return false;
+      const T g = T(1e-5);
+      return cmp_le(tht, (T(1) - g) * th, th) || cmp_le(pht - ph, -g * th, ph);
+    };
     T alpha = a0, ph_acc = ph, a_test = a0, th_t = T(0), ph_t = T(0);
     int nls = nls0, ntr = 0;
     int flags = 0;
@@ -2308,8 +2318,8 @@ struct WaveSolver {
         if (fin) {
           ok = th_t <= theta_max;
           if (ok) {
-            if (a_test > T(0) && is_ftype(a_test, ref) && th <= theta_min) ok = armijo(ph_t, a_test, ref);
-            else ok = acc_to_iterate(th_t, ph_t, ref);
+            if (a_test > T(0) && ftype(a_test) && th <= theta_min) ok = armijo(ph_t, a_test, ref);
+            else ok = acc_it(th_t, ph_t);
           }
           if (ok && !filter_ok(th_t, ph_t)) { ok = false; flags |= LSR_REJF; }
         }
@@ -2318,7 +2328,7 @@ struct WaveSolver {
 #endif
         if (wuni(w, ok)) {
           flags |= LSR_ACC | LSR_FIN;
-          if (!(is_ftype(a_test, ref) && armijo(ph_t, a_test, ref))) flags |= LSR_AUG;
+          if (!(ftype(a_test) && armijo(ph_t, a_test, ref))) flags |= LSR_AUG;
           ph_acc = ph_t;
           store = true;
           break;
