@@ -502,6 +502,10 @@ int mr_create(mr_handle** out, const mr_config* cfg) {
   if (cfg->model < 0 || cfg->model > 4) return fail(MR_ERR_ARG, "unknown model");
   if (cfg->precision != MR_PREC_FP64 && cfg->precision != MR_PREC_FP32) return fail(MR_ERR_ARG, "bad precision");
   if (cfg->max_batch < 1) return fail(MR_ERR_ARG, "max_batch < 1");
+  // the line-search filter holds FCAP entries (mr_solver.h): at most one per iteration plus the restoration
+  // entry's, so a solve with max_iter <= FCAP - 2 never drops one (IPOPT's filter is unbounded)
+  if (cfg->max_iter < 0 || cfg->max_iter > FCAP - 2)
+    return fail(MR_ERR_ARG, "max_iter out of range (0.." + std::to_string(FCAP - 2) + ": the line-search filter's capacity)");
   if (!(cfg->Ts > 0)) return fail(MR_ERR_ARG, "Ts must be > 0");
   if (cfg->dispatch_order < 0 || cfg->dispatch_order > 2) return fail(MR_ERR_ARG, "dispatch_order must be 0, 1 or 2");
   {

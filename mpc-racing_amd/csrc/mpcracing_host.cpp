@@ -78,6 +78,7 @@ int mrh_solve_batch(const mr_config* c, const double* a_front, double Fz_front, 
   TyreCoef<double> tf{}, tr{};
   if (a_front) tf = pacejka_coef(a_front, Fz_front);
   if (a_back) tr = pacejka_coef(a_back, Fz_back);
+  if (c->max_iter < 0 || c->max_iter > FCAP - 2) return -1;  // the line-search filter's capacity (mr_create)
 #define MR_CASE(T, M) run<T, M>(*c, tf, tr, B, *in, *out, nthreads)
 #define MR_MODELS(T)                                                       \
   switch (c->model) {                                                      \
@@ -99,6 +100,7 @@ int mrh_solve_batch_scalar(const mr_config* c, const double* a_front, double Fz_
   if (a_front) tf = pacejka_coef(a_front, Fz_front);
   if (a_back) tr = pacejka_coef(a_back, Fz_back);
   if (c->N < 1 || c->N > 63) return -1;
+  if (c->max_iter < 0 || c->max_iter > FCAP - 2) return -1;
 #define MR_CASE(T, M) run_scalar<T, M>(*c, tf, tr, B, *in, *out, nthreads)
   if (c->precision == MR_PREC_FP64) { MR_MODELS(double) } else { MR_MODELS(float) }
 #undef MR_CASE

@@ -829,6 +829,7 @@ struct Solver {
   T ofilt_th[FCAP], ofilt_ph[FCAP];
   int onfilt;
   T tho_acc, pho_acc;  // original theta / barrier objective of the last trial point (restoration)
+  T fo_acc = T(0), fo_cur = T(0);  // original (scaled) objective of the last trial point / the current iterate
   bool have_acc = false;  // an acceptable iterate is stored (AZ)
   bool resto_first = false;  // the restoration phase's first iteration (no barrier update)
   double* trace = nullptr;  // optional per-iteration record (diagnostics)
@@ -1847,6 +1848,7 @@ struct Solver {
     ph_t = fv - mu * (lg + lgr) + kdm * lin;
     if (resto) {  // the point measured as the original problem sees it (restoration exit test)
       tho_acc = tho;
+      fo_acc = fo;
       pho_acc = fo - mu_o * lg + T(IP_KAPPA_D) * mu_o * lin;
     }
     if (!(th_t == th_t) || !(ph_t == ph_t)) ok = false;
@@ -2065,6 +2067,7 @@ struct Solver {
     // sweep's (defects W(k, C), pr_max, theta) belong to the abandoned iterate.  IPOPT's
     // RestoIterateInitializer: mu_r = max(mu, ||c||_inf, ||d - s||_inf)
     T pr = T(0), th_r = T(0);
+    fo_cur = T(0);  // the original objective at the entry point (reported if the restoration phase ends the solve)
     for (int k = 0; k <= N; ++k) {
       T z[NZS];
       load_z(k, cur, z);
@@ -2087,6 +2090,7 @@ struct Solver {
       row_values(k, z, e, d, act, rows);
       for (int j = 0; j < NI; ++j)
         if (act[j] && yslot(j)) pr = mr_max(pr, mr_abs(d[j] - W(k, sf(cur) + j)));
+      fo_cur += stage_cost(P, I, k, z, e, sc, (T*)nullptr, (T*)nullptr);
     }
     const T mu_r = mr_max(mu, pr);
     for (int k = 0; k <= N; ++k) {
@@ -2452,6 +2456,7 @@ struct Solver {
         bool soc_taken;
         const bool accepted = backtrack(ap, false, false, T(0), ref, a_min, alpha, a_test, ph_acc, nls, soc_taken);
         if (!accepted) { out.status = 3; break; }  // IPOPT: restoration failed
+        fo_cur = fo_acc;  // the accepted step's point is the last trial evaluated (no SOC here)
         for (int k = 0; k <= N; ++k) {
           for (int j = 0; j < NI; ++j) {
             W(k, WF::RP + j) += alpha * W(k, WF::RDP + j);
@@ -2624,6 +2629,8 @@ struct Solver {
       cur = 1 - cur;
     }
     out.iters = it;
+    // ended inside the restoration phase: the returned (restoration) iterate's original objective
+    if (resto) out.obj = (double)(fo_cur / sc);
     if (trace && it < trace_cap) {  // final record: why the loop ended
       double* tr = trace + 8 * it;
       tr[0] = (double)out.kkt; tr[1] = (double)fval; tr[2] = (double)theta; tr[3] = (double)stat_max;

@@ -64,39 +64,9 @@
 #ifndef MR_PHASE_CYCLES
 #define MR_PHASE_CYCLES 0  // 1: per-sweep shader-cycle counters of the trace instance (tools/phase_probe.py)
 #endif
-#ifndef MR_EVAL_HOIST
-#define MR_EVAL_HOIST 0  // 1: the evaluation sweep loads slacks / multipliers ahead of the record stores
-#endif
-#ifndef MR_FWD_TREE
-#define MR_FWD_TREE 0  // 1: the forward recursion's dot products as three chains (A/B option)
-#endif
-#ifndef MR_RIC_AHEAD
-#define MR_RIC_AHEAD 2  // stages the Riccati's operand gathers run ahead of the factorisation (2 or 3)
-#endif
-#ifndef MR_MFMA_CHAIN
-#define MR_MFMA_CHAIN 0  // 1: the forward / SOC recursions as MFMA products of the closed-loop map (A/B option: slower)
-#endif
-#ifndef MR_MFMA_SOCB
-#define MR_MFMA_SOCB 2  // the SOC costate pass on stage-parallel v_k, u_k: 2 the lane recursion forming A^T pv + K^T B^T pv (socb_chain); A/B options: 3 the lane recursion on a stored closed-loop map (socb_chain_acl: its chain 45 % shorter, the batch 2.3 % slower -- profiles/r05_socb_ab.json), 1 the MFMA chain, 0 the lane-group recursion
-#endif
-#ifndef MR_FWD_UNROLL6
-#define MR_FWD_UNROLL6 0  // 1: the forward recursion unrolled by six (A/B option)
-#endif
-#ifndef MR_EVAL_BRANCHFREE
-#define MR_EVAL_BRANCHFREE 0  // 1: the evaluation sweep's slot loop and row_steps branch-free (A/B option: 96.2 vs 91.5 ms -- every slot's fields loaded and stored, profiles/r05_eval_branchfree_ab.json)
-#endif
-#ifndef MR_LS_BRANCHFREE
-#define MR_LS_BRANCHFREE 1  // the trial evaluation's slot loop without per-slot branches
-#endif
-#ifndef MR_SOC_GPRE
-#define MR_SOC_GPRE 0  // 1: the SOC costate pass's fixed gradient terms stored once per SOC episode (A/B option: 93.5 vs 92.5 ms, profiles/r05_riccati_pick_ab.json)
-#endif
-#ifndef MR_SOC_CAPTURE
-#define MR_SOC_CAPTURE 1  // a SOC trial point's constraint values captured by its evaluation (LS_CAP), not re-evaluated
-#endif
-#ifndef MR_PRIO_ITER
-#define MR_PRIO_ITER 0  // > 0: the wave raises its issue priority (s_setprio) at this iteration
-#endif
+// trace rows reserved at the end of a trace buffer: the final status record's slack row and the cycle rows
+// (MR_PHASE_CYCLES: rows trace_cap - 1 .. trace_cap - 3), never overwritten by per-iteration rows
+#define MR_TRACE_RESERVED (MR_PHASE_CYCLES ? 3 : 2)
 
 namespace mr {
 
@@ -130,15 +100,9 @@ struct RCF {
     JUNK, NF                           // discard slot of the branch-free stores (any lane)
   };
 };
-#ifdef MR_RC_STRIDE_FORCE
-constexpr int RC_STRIDE = MR_RC_STRIDE_FORCE;  // A/B option (record footprint)
-#else
 constexpr int RC_STRIDE = (RCF::NF + 15) / 16 * 16;  // words; 16-word (64 B) multiple (304)
-#endif
 static_assert(RCF::NF <= RC_STRIDE, "record");
-#ifndef MR_RC_STRIDE_FORCE
 static_assert(RC_STRIDE == 304, "record stride (DESIGN.md §3)");
-#endif
 // Cold per-stage fields [f][64] after the records: touched only by the watchdog (its snapshot of the
 // iterate and the search direction) and the restoration phase (the relaxations p, n of the rows and
 // of the 6 vehicle dynamics rows, their bound duals and steps, the rows' equality multipliers y, the
@@ -160,11 +124,7 @@ struct CSF {
     // a trial point's constraint values captured for the second-order correction that may follow it
     // (LS_CAP): the rows' (d - s) (NI) and the dynamics defects (NX), 0 where none is accumulated
     CTR = CGW1 + 6, CTC = CTR + NI,
-    // the SOC costate pass's gradient terms that stay fixed over an SOC episode (soc_prepare): the base
-    // G0 + mu G1 + delta GD, per row (c0, c1, e0, e1) with dg = c0 (SR0 - e0) + c1 (SR1 + e1), the lane
-    // row's e_C gradient
-    SGB = CTC + NX, SGR = SGB + NZ, SGC = SGR + 4 * (NROW + 1),
-    SJUNK = SGC + 3,  // discard slot of the SOC chains' lanes without a component
+    SJUNK = CTC + NX,  // discard slot of the SOC chains' lanes without a component
     // the filter's entries beyond the FMAX in LDS (mr_solver.h FCAP): [bank][theta | phi][FOVF] fields, entry
     // FMAX + 64 q + l in lane l of field q; bank 0 the original problem's, bank 1 the restoration phase's
     FOV = SJUNK + 1,
@@ -175,12 +135,8 @@ struct CSF {
 // the solve precision, [3][NX][64] doubles after the cold fields: eval_sweep forms the stationarity residual and the
 // Riccati right-hand side from them in fp64 (the correction form, see there).
 constexpr int64_t WS_NU_OFF = (int64_t)SSF::NF * WL + (int64_t)RC_STRIDE * WL + (int64_t)CSF::NF * WL;  // words
-// The closed-loop map of the accepted factorisation for the second-order corrections' costate pass
-// (MR_MFMA_SOCB 3): field i NX + j, lane k holds Acl_k[j][i] (Acl = A + B K), after the multipliers.
 template <typename T>
-MR_HD constexpr int64_t ws_mt_off() { return WS_NU_OFF + 3 * NX * WL * (int64_t)(sizeof(double) / sizeof(T)); }
-template <typename T>
-MR_HD constexpr int64_t ws_words() { return ws_mt_off<T>() + (MR_MFMA_SOCB == 3 ? (int64_t)NX * NX * WL : 0); }
+MR_HD constexpr int64_t ws_words() { return WS_NU_OFF + 3 * NX * WL * (int64_t)(sizeof(double) / sizeof(T)); }
 
 // Wave-uniform state of the watchdog and the restoration phase: one copy per wavefront next to the
 // line-search filter (LDS on the device), every lane writing the same values -- not in the per-lane
@@ -189,6 +145,7 @@ template <typename T>
 struct WaveCold {
   int resto, in_wd, wd_short, wd_trial, onfilt, mrow, have_acc, tiny, resto_first, in_soft, soft_count;
   T rho, zeta, mu_o, th_entry, delta_last_o, theta_max_o, theta_min_o, tho, pho;
+  T fo, fo_cur;  // restoration: the original (scaled) objective of the last trial point / of the current iterate
   T wd_th, wd_ph, wd_gphi, wd_ap, wd_ad, wd_amin, wd_thpow;
   // evaluation aggregates beyond the solver object's (mr_solver.h Solver): primal infeasibility of the
   // equality rows, bound violation of the rows, |y|_1, the damped slacks' sum, the original problem's
@@ -360,7 +317,6 @@ struct WaveSolver {
   MR_HD MR_GLOBAL double& NUd(int i) const { return nub()[i * WL + ln]; }
   MR_HD MR_GLOBAL double& WNUd(int i) const { return nub()[(NX + i) * WL + ln]; }
   MR_HD MR_GLOBAL double& ANUd(int i) const { return nub()[(2 * NX + i) * WL + ln]; }  // acceptable-point copy
-  MR_HD MR_GLOBAL T* mtb() const { return rc - (int64_t)SSF::NF * WL + ws_mt_off<T>(); }  // Acl fields
   MR_HD auto& fth(int i) const { return filt[i]; }
   MR_HD auto& fph(int i) const { return filt[FMAX + i]; }
   MR_HD MR_GLOBAL T* R(int k) const { return rc + (int64_t)k * RC_STRIDE; }
@@ -783,48 +739,7 @@ struct WaveSolver {
       row_values(k, z, e, d, act);
       T lam_j[NI], s_j[NI];
       T sg_j[NI], c0_j[NI], c1_j[NI], y_j[NI];  // restoration: condensed row data (row_cond_r), multipliers y
-#if MR_EVAL_BRANCHFREE
-      if constexpr (!RESTO) {
-        // branch-free over the slots: an inactive slot's operands are replaced (s = 1), its terms selected
-        // out and its multipliers written back unchanged -- the same sums and fields as the branching form
-#pragma unroll
-        for (int j = 0; j < NI; ++j) {
-          const bool a = act[j] != 0;
-          sg_j[j] = c0_j[j] = c1_j[j] = T(0);
-          const T sv = S(sf(cur) + j), lv = S(SSF::LAM + j), dlv = S(SSF::DLAM + j);
-          const T s = a ? sv : T(1);
-          T lam = lv + alpha_d * dlv;
-          lam = mr_min(mr_max(lam, mu_prev / (kappa_sigma * s)), kappa_sigma * mu_prev / s);
-          lam = a ? lam : lv;
-          S(SSF::LAM + j) = lam;
-          lam_j[j] = a ? lam : T(0);
-          s_j[j] = s;
-          const T rd = d[j] - s;
-          const T sl = s * lam;
-          smax_l = a ? mr_max(smax_l, sl) : smax_l;
-          smin_l = a ? mr_min(smin_l, sl) : smin_l;
-          lam1_l += a ? mr_abs(lam) : T(0);
-          lg_l += a ? mr_log(s) : T(0);
-          mi_l += a ? 1 : 0;
-          viol_l = a ? mr_max(viol_l, -d[j]) : viol_l;
-          if (oneslot(j)) lin_l += a ? s : T(0);
-          y_j[j] = T(0);
-          if (yslot(j)) {
-            pro_l = a ? mr_max(pro_l, mr_abs(rd)) : pro_l;
-            const T yv = S(SSF::Y + j);
-            const T y = a ? yv + alpha_p * S(SSF::DY + j) : yv;
-            S(SSF::Y + j) = y;
-            y_j[j] = a ? y : T(0);
-            y1_l += a ? mr_abs(y) : T(0);
-            mrow_l += a ? 1 : 0;
-            pr_l = a ? mr_max(pr_l, mr_abs(rd)) : pr_l;
-            th_l += a ? mr_abs(rd) : T(0);
-          }
-        }
-      }
-#endif
       for (int j = 0; j < NI; ++j) {
-        if (MR_EVAL_BRANCHFREE && !RESTO) break;
         lam_j[j] = T(0);
         s_j[j] = T(1);
         sg_j[j] = c0_j[j] = c1_j[j] = y_j[j] = T(0);
@@ -1273,10 +1188,6 @@ struct WaveSolver {
     T raw_a[NGATHER], raw_b[NGATHER], raw_c[NGATHER];
     frag_load<DS>(rb, R(N - 1), fp, raw_a);
     frag_load<DS>(rb, R(N >= 2 ? N - 2 : 0), fp, raw_b);
-#if MR_RIC_AHEAD == 3
-    T raw_d[NGATHER];
-    frag_load<DS>(rb, R(N >= 3 ? N - 3 : 0), fp, raw_c);
-#endif
     {  // terminal cost-to-go: P_N = H_N,xx + delta I, p_N = g_N.  Branch-free (lanes >= NX write
        // discard slots), so at least as many memory ops follow the first prefetch on this path as
        // on the loop back-edge and the wait at the loop head stays exact.
@@ -1313,7 +1224,7 @@ struct WaveSolver {
       frag_finish<DS>(dd, delta, raw_use, eb, dq);
 #pragma unroll
       for (int v = 0; v < 4; ++v) dq[v] = (dq[v] + s14 * wrow_next(w, dq[v])) * k15;  // g0 + mu g1 | 0
-      frag_load<DS>(rb, (unsigned)wu(w, (int)R(k >= MR_RIC_AHEAD ? k - MR_RIC_AHEAD : 0)), fp, raw_fill);  // unconditional: k < AHEAD re-read stage 0's record
+      frag_load<DS>(rb, (unsigned)wu(w, (int)R(k >= 2 ? k - 2 : 0)), fp, raw_fill);  // unconditional: k < 2 re-read stage 0's record
       // X = P^ E^  (A fragment s: P^[c][4s+g])
       // two independent 2-MFMA accumulation chains (k = 0..7 | 8..15) instead of one 4-long
       // dependent chain: half the MFMA latency on the stage's critical path
@@ -1382,20 +1293,6 @@ struct WaveSolver {
     // next two, and the loop keeps one back-edge block (exact prefetch waits at the loop head).
     // Buffer roles rotate a -> c -> b -> a over the three unrolled steps.
     bool ok = true;
-#if MR_RIC_AHEAD == 3
-    // A/B option: gathers three stages ahead, four rotating buffers (a -> d -> c -> b -> a)
-    for (int k = N - 1;; k -= 4) {
-      ok = step(k, raw_a, raw_d) & ok;
-      if (k == 0) break;
-      ok = step(k - 1, raw_b, raw_a) & ok;
-      if (k == 1) break;
-      ok = step(k - 2, raw_c, raw_b) & ok;
-      if (k == 2) break;
-      ok = step(k - 3, raw_d, raw_c) & ok;
-      if (k == 3) break;
-      if (!wuni(w, ok)) return false;
-    }
-#else
     for (int k = N - 1;; k -= 3) {
       ok = step(k, raw_a, raw_c) & ok;
       if (k == 0) break;
@@ -1405,7 +1302,6 @@ struct WaveSolver {
       if (k == 2) break;
       if (!wuni(w, ok)) return false;
     }
-#endif
     if (!wuni(w, ok)) return false;
     wsync(w);  // records (P, p, K, k) visible to every lane
     return true;
@@ -1480,21 +1376,8 @@ struct WaveSolver {
       auto fstep = [&](int k, const FwdRow& f) {
         T dxv[NX];
         wgather<T, NX>(w, dxi, dxv);
-#if MR_FWD_TREE
-        // the 11-term dot as three interleaved chains (critical path 4 FMAs + 2 adds, not 11)
-        T a0 = f.c0, a1 = f.rw[1] * dxv[1], a2 = f.rw[2] * dxv[2];
-        a0 += f.rw[0] * dxv[0];
-#pragma unroll
-        for (int j = 3; j < NX; j += 3) {
-          a0 += f.rw[j] * dxv[j];
-          if (j + 1 < NX) a1 += f.rw[j + 1] * dxv[j + 1];
-          if (j + 2 < NX) a2 += f.rw[j + 2] * dxv[j + 2];
-        }
-        const T acc = (a0 + a1) + a2;
-#else
         T acc = f.c0;
         for (int j = 0; j < NX; ++j) acc += f.rw[j] * dxv[j];
-#endif
         // dx_{k+1} = (A dx_k + c) + B du_k on group 0, du_k from group 2 (lanes 32..34)
         T accx = acc;
 #pragma unroll
@@ -1513,30 +1396,6 @@ struct WaveSolver {
       FwdRow fa, fb, fc;
       fload(0, fa);
       fload(1, fb);
-#if MR_FWD_UNROLL6
-      // unrolled by six over the three sets: the compiler's wait at the loop head (its merge of the
-      // back-edge state is conservative, vmcnt drains the older set too) hits one step in six, not three
-      for (int k = 0;; k += 6) {
-        fload(k + 2, fc);
-        fstep(k, fa);
-        if (k == N) break;
-        fload(k + 3, fa);
-        fstep(k + 1, fb);
-        if (k + 1 == N) break;
-        fload(k + 4, fb);
-        fstep(k + 2, fc);
-        if (k + 2 == N) break;
-        fload(k + 5, fc);
-        fstep(k + 3, fa);
-        if (k + 3 == N) break;
-        fload(k + 6, fa);
-        fstep(k + 4, fb);
-        if (k + 4 == N) break;
-        fload(k + 7, fb);
-        fstep(k + 5, fc);
-        if (k + 5 == N) break;
-      }
-#else
       for (int k = 0;; k += 3) {
         fload(k + 2, fc);
         fstep(k, fa);
@@ -1548,274 +1407,12 @@ struct WaveSolver {
         fstep(k + 2, fc);
         if (k + 2 == N) break;
       }
-#endif
       wsync_lds(w);
       if (ln <= N)
         for (int j = 0; j < NX; ++j) dz[j] = LDX[ln * 12 + j];
       if (ln < N)
         for (int a = 0; a < NU; ++a) dz[NX + a] = lds[LX_OFF + 3 * ln + a];
     }
-  }
-
-  // ---------------- the closed-loop recursions on the matrix cores ----------------
-  // Given the factorisation (gains K_k, feed-forward kff_k), the forward substitution is the affine recursion
-  //   dx_{k+1} = Acl_k dx_k + w_k,   Acl = A + B K,  w = B kff + c   (dx_0 = 0),
-  // and a second-order correction's costate pass (soc_backward) is its transpose
-  //   pv_k = Acl_k^T pv_{k+1} + v_k.
-  // Each runs as one 16x16x4 MFMA product per stage on the augmented vector y = [x; 1] (rows 0..11):
-  //   y_{k+1} = M_k y_k,  M_k = [Acl_k | w_k ; 0 | 1]   (TR: y_k = M_k y_{k+1} with [Acl_k^T | v_k ; 0 | 1]),
-  // every column of the B operand a copy of y, three K-chunks (columns 0..11), the D result turned into
-  // the next B operand in registers (wtranspose4; fp64's D layout already is).  M_k's entries are formed
-  // per lane from the stage record -- entry (i, j) = base + p1 x1 + p2 x2, A + B K's structure: the vehicle
-  // rows' Jacobian J and the gains, the S / previous-control / frozen-copy rows' 0/1 entries from the
-  // record's constant slots (m_terms) -- gathered two stages ahead, so nothing beyond the Riccati's record
-  // is stored.  The critical path per stage is 3 MFMAs and 4 permutes instead of an 11-value broadcast
-  // and an 11-term dot (fwd_recursion's lane-group recursion, MR_MFMA_CHAIN=0).
-  // record offsets of entry (r, col) of M = [A + B K | B kff + c ; 0 | 1] (col 11: the affine column)
-  static MR_HD void m_terms(int r, int col, unsigned* t) {  // t = {base, p1, x1, p2, x2}
-    const unsigned Z = RCF::CZERO, O = RCF::CONE;
-    for (int q = 0; q < 5; ++q) t[q] = Z;
-    if (r >= 12 || col >= 12) return;
-    if (r == 11) { t[0] = col == 11 ? O : Z; return; }
-    const bool aff = col == 11;
-    auto kx = [&](int a) -> unsigned { return aff ? (unsigned)(RCF::K0 + a) : (unsigned)(RCF::K + a * NX + col); };
-    if (r < 6) {  // vehicle rows: J[r][col] (col < 6) + J[r][6] K[0][col] + J[r][7] K[1][col]
-      t[0] = aff ? RCF::C + r : (col < 6 ? RCF::J + r * 8 + col : Z);
-      t[1] = RCF::J + r * 8 + 6; t[2] = kx(0);
-      t[3] = RCF::J + r * 8 + 7; t[4] = kx(1);
-    } else if (r == 6) {  // S+ = S + dS
-      t[0] = aff ? RCF::C + 6 : (col == 6 ? O : Z); t[1] = O; t[2] = kx(2);
-    } else if (r == 7 || r == 8) {  // p+ = (thr, steer)
-      t[0] = aff ? RCF::C + r : Z; t[1] = O; t[2] = kx(r - 7);
-    } else {  // w+ = w (k > 0) or (thr, steer) (k = 0)
-      t[0] = aff ? RCF::C + r : (col == r ? RCF::SELP : Z); t[1] = RCF::SEL0; t[2] = kx(r - 9);
-    }
-  }
-  struct ChainRaw {
-    T t[3][5];  // the three fragments' gathered terms
-    T c[3];     // the affine column's cold replacements (SOCM: c_soc, k_soc; TR: v_k)
-  };
-  // TR: the transposed (costate) recursion, backward in k, v_k from the cold field SPV; SOCM: the affine
-  // column from the SOC's cold fields (c_soc in SC, k_soc in SK0).  Result rows y to LDX[row k] (TR) or
-  // [row k + 1] (forward); the caller provides the start y0 (forward: dx_0 = 0; TR: pv_N) as B-operand rows.
-  // The loop body only gathers (two stages ahead, three rotating register sets, exits at step ends: no
-  // register copies of in-flight loads), multiplies and writes LDS -- no global stores, whose completion
-  // the in-order vmcnt would make the next gather's wait include.
-  template <bool TR, bool SOCM>
-  MR_HD void mfma_chain(const T* y0) {
-    const int N = wu(this->w, this->N), ln = this->ln;
-    const Wv w = this->w;
-    const WBuf<T> wb(rc - (int64_t)SSF::NF * WL, (unsigned)WS_NU_OFF);
-    auto R = [](int k) { return (unsigned)(SSF::NF * WL) + (unsigned)k * (unsigned)RC_STRIDE; };
-    const unsigned cold0 = (unsigned)(SSF::NF * WL) + (unsigned)RC_STRIDE * WL;
-    MR_LDS T* const LDX = lds + LDX_OFF;
-    const int i = ln & 15, g = ln >> 4;
-    unsigned off[3][5];
-    for (int s = 0; s < 3; ++s) {
-      const int j = 4 * s + g;
-      if (!TR) {
-        m_terms(i, j, off[s]);
-      } else {
-        for (int q = 0; q < 5; ++q) off[s][q] = RCF::CZERO;
-        if (i < 11 && j < 11) m_terms(j, i, off[s]);
-        else if (i == 11 && j == 11) off[s][0] = RCF::CONE;
-      }
-    }
-    // the affine column (lanes g = 3 of fragment 2, rows i < 11): its cold replacements
-    const bool aff = (SOCM || TR) && g == 3 && i < 11;
-    unsigned coff[3] = {(unsigned)CSF::SJUNK * WL, (unsigned)CSF::SJUNK * WL, (unsigned)CSF::SJUNK * WL};
-    if (aff) {
-      if (TR) {
-        coff[0] = (unsigned)(CSF::SPV + i) * WL;
-      } else {
-        const int a1 = i < 6 ? 0 : (i == 6 ? 2 : (i == 7 || i == 9 ? 0 : 1));
-        coff[0] = (unsigned)(CSF::SC + i) * WL;
-        coff[1] = (unsigned)(CSF::SK0 + a1) * WL;
-        coff[2] = (unsigned)(CSF::SK0 + 1) * WL;  // (x2 = kff[1] on the vehicle rows; p2 = 0 elsewhere)
-      }
-    }
-    auto cload = [&](int kk, ChainRaw& r) {
-      kk = kk < 0 ? 0 : (kk < N ? kk : N - 1);
-      const unsigned ro = (unsigned)wu(w, (int)R(kk));
-#pragma unroll
-      for (int s = 0; s < 3; ++s)
-#pragma unroll
-        for (int q = 0; q < 5; ++q) r.t[s][q] = wb.ld(ro, off[s][q]);
-      if constexpr (SOCM || TR) {
-        const unsigned co = (unsigned)wu(w, (int)(cold0 + (unsigned)kk));
-#pragma unroll
-        for (int q = 0; q < 3; ++q) r.c[q] = (TR && q > 0) ? T(0) : wb.ld(co, coff[q]);
-      }
-    };
-    // B operand: xb[s] = y[4s + g]
-    T xb[4] = {y0[0], y0[1], y0[2], T(0)};
-    const bool wr = (ln & 15) == 0;
-    auto cstep = [&](int k, const ChainRaw& r) {
-      T fr[3];
-#pragma unroll
-      for (int s = 0; s < 3; ++s) fr[s] = r.t[s][0] + r.t[s][1] * r.t[s][2] + r.t[s][3] * r.t[s][4];
-      if constexpr (TR) {
-        fr[2] = aff ? r.c[0] : fr[2];
-      } else if constexpr (SOCM) {
-        fr[2] = aff ? r.c[0] + r.t[2][1] * r.c[1] + r.t[2][3] * r.c[2] : fr[2];
-      }
-      T d[4] = {T(0), T(0), T(0), T(0)}, d2[4] = {T(0), T(0), T(0), T(0)};
-      wmfma(w, fr[0], xb[0], d);
-      wmfma(w, fr[2], xb[2], d2);
-      wmfma(w, fr[1], xb[1], d);
-#pragma unroll
-      for (int v = 0; v < 4; ++v) d[v] += d2[v];
-      const int orow = TR ? k : k + 1;
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int row = drow(g, v);
-        LDX[(wr && row < 12) ? orow * 12 + row : LJUNK_OFF - LDX_OFF + ln] = d[v];
-      }
-#pragma unroll
-      for (int v = 0; v < 4; ++v) xb[v] = d[v];
-      if constexpr (sizeof(T) == 4) wtranspose4(w, xb);
-    };
-    // (scheduling barriers keep each prefetch ahead of the step that follows it: without them the
-    // scheduler sank the gathers to the back-edge and every step waited out a memory round trip)
-    ChainRaw ra, rb2, rc2;
-    if constexpr (!TR) {
-      cload(0, ra);
-      cload(1, rb2);
-      for (int k = 0;; k += 3) {
-        cload(k + 2, rc2);
-        MR_SCHED_BARRIER();
-        cstep(k, ra);
-        if (k + 1 == N) break;
-        cload(k + 3, ra);
-        MR_SCHED_BARRIER();
-        cstep(k + 1, rb2);
-        if (k + 2 == N) break;
-        cload(k + 4, rb2);
-        MR_SCHED_BARRIER();
-        cstep(k + 2, rc2);
-        if (k + 3 == N) break;
-      }
-    } else {
-      cload(N - 1, ra);
-      cload(N - 2, rb2);
-      for (int k = N - 1;; k -= 3) {
-        cload(k - 2, rc2);
-        MR_SCHED_BARRIER();
-        cstep(k, ra);
-        if (k == 0) break;
-        cload(k - 3, ra);
-        MR_SCHED_BARRIER();
-        cstep(k - 1, rb2);
-        if (k == 1) break;
-        cload(k - 4, rb2);
-        MR_SCHED_BARRIER();
-        cstep(k - 2, rc2);
-        if (k == 2) break;
-      }
-    }
-    wsync_lds(w);
-  }
-
-  // After the forward recursion (dx_k in LDX rows): per stage, independent of the others, the product
-  // G_k [dx_k; 1] with G_k = [P_k | p_k ; K_k | kff_k] (rows 0..10: the costate step dnu_k; rows 11..13: du_k;
-  // SOCM: the SOC's costate vector and k_soc from the cold fields), on the MFMA with the same lane maps;
-  // every lane gathers from the same stage record (a few cache lines per gather), two stages ahead.
-  // dnu_k to its stage field (SSF::DNU; SOCM: the cold SDNU), du_k to LDS (LX_OFF + 3 k + a).
-  template <bool SOCM>
-  MR_HD void gpass() {
-    const int N = wu(this->w, this->N), ln = this->ln;
-    const Wv w = this->w;
-    const WBuf<T> wb(rc - (int64_t)SSF::NF * WL, (unsigned)WS_NU_OFF);
-    auto R = [](int k) { return (unsigned)(SSF::NF * WL) + (unsigned)k * (unsigned)RC_STRIDE; };
-    const unsigned cold0 = (unsigned)(SSF::NF * WL) + (unsigned)RC_STRIDE * WL;
-    MR_LDS T* const LDX = lds + LDX_OFF;
-    const int i = ln & 15, g = ln >> 4;
-    unsigned goff[3], xoff[3];
-    for (int s = 0; s < 3; ++s) {
-      const int j = 4 * s + g;
-      goff[s] = (i < NX) ? (j < NX ? (unsigned)(RCF::P + pidx(i, j)) : (j == 11 ? (unsigned)(RCF::PV0 + i) : (unsigned)RCF::CZERO))
-                         : (i < NX + NU ? (j < NX ? (unsigned)(RCF::K + (i - NX) * NX + j)
-                                                  : (j == 11 ? (unsigned)(RCF::K0 + i - NX) : (unsigned)RCF::CZERO))
-                                        : (unsigned)RCF::CZERO);
-      xoff[s] = (unsigned)j;  // B operand row j of y_k = [dx_k; 1] (LDX row k, element 11 set below)
-    }
-    const bool gaff = SOCM && g == 3 && i < NX + NU;  // G's affine column from the SOC's cold fields
-    const unsigned gcoff = gaff ? (unsigned)((i < NX ? CSF::SPV + i : CSF::SK0 + i - NX) * WL) : (unsigned)CSF::SJUNK * WL;
-    struct GRaw {
-      T q[3], c;
-    };
-    auto gload = [&](int kk, GRaw& r) {
-      kk = kk < N ? kk : N;
-      const unsigned ro = (unsigned)wu(w, (int)R(kk));
-#pragma unroll
-      for (int s = 0; s < 3; ++s) r.q[s] = wb.ld(ro, goff[s]);
-      if constexpr (SOCM) r.c = wb.ld((unsigned)wu(w, (int)(cold0 + (unsigned)kk)), gcoff);
-    };
-    const bool wr = (ln & 15) == 0;
-    auto gstep = [&](int k, const GRaw& r) {
-      T gf[3] = {r.q[0], r.q[1], r.q[2]};
-      if constexpr (SOCM) gf[2] = gaff ? r.c : gf[2];
-      T xb[3];
-#pragma unroll
-      for (int s = 0; s < 3; ++s) xb[s] = xoff[s] < 11 ? LDX[k * 12 + xoff[s]] : (xoff[s] == 11 ? T(1) : T(0));
-      T e[4] = {T(0), T(0), T(0), T(0)}, e2[4] = {T(0), T(0), T(0), T(0)};
-      wmfma(w, gf[0], xb[0], e);
-      wmfma(w, gf[2], xb[2], e2);
-      wmfma(w, gf[1], xb[1], e);
-#pragma unroll
-      for (int v = 0; v < 4; ++v) e[v] += e2[v];
-      const bool dn = k >= 1 || !MR_KKT_RESTATED;  // k = 0: the initial-state rows' multiplier step
-      const unsigned ku = (unsigned)wu(w, k), junk = R(k) + RCF::JUNK - ku;  // (stage k's record discard slot)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int row = drow(g, v);
-        const bool st = wr && row < NX && dn;
-        if constexpr (SOCM) {
-          wb.st(e[v], ku, st ? cold0 + (unsigned)(CSF::SDNU + row) * WL : junk);
-        } else if constexpr (SSL) {
-          if (st) ss[(SSF::DNU + row) * WL + k] = e[v];
-        } else {  // branch-free: other lanes write the discard slot
-          wb.st(e[v], ku, st ? (unsigned)(SSF::DNU + row) * WL : junk);
-        }
-        lds[(wr && row >= NX && row < NX + NU && k < N) ? LX_OFF + 3 * k + row - NX : LJUNK_OFF + ln] = e[v];
-      }
-    };
-    GRaw ga, gb, gc;
-    gload(0, ga);
-    gload(1, gb);
-    for (int k = 0;; k += 3) {
-      gload(k + 2, gc);
-      MR_SCHED_BARRIER();
-      gstep(k, ga);
-      if (k == N) break;
-      gload(k + 3, ga);
-      MR_SCHED_BARRIER();
-      gstep(k + 1, gb);
-      if (k + 1 == N) break;
-      gload(k + 4, gb);
-      MR_SCHED_BARRIER();
-      gstep(k + 2, gc);
-      if (k + 2 == N) break;
-    }
-    wsync_lds(w);
-  }
-
-  // the forward substitution by mfma_chain (dx_k to LDX rows), then gpass (dnu_k to its field, du_k to LDS),
-  // then this lane's stage direction dz (SOCM: the SOC's kff / costate vector, dnu into SDNU)
-  template <bool SOCM>
-  MR_HD void fwd_chain(T* dz) {
-    const int N = wu(this->w, this->N);
-    MR_LDS T* const LDX = lds + LDX_OFF;
-    const int g = ln >> 4;
-    T y0[3];
-    for (int s = 0; s < 3; ++s) y0[s] = (4 * s + g == 11) ? T(1) : T(0);
-    if (ln < 12) LDX[ln] = T(0);  // dx_0 = 0
-    mfma_chain<false, SOCM>(y0);
-    gpass<SOCM>();
-    if (ln <= N)
-      for (int j = 0; j < NX; ++j) dz[j] = LDX[ln * 12 + j];
-    if (ln < N)
-      for (int a = 0; a < NU; ++a) dz[NX + a] = lds[LX_OFF + 3 * ln + a];
   }
 
   // ---------------- sweep 3: forward substitution, slack/dual steps ----------------
@@ -1833,11 +1430,7 @@ struct WaveSolver {
     const T tau = mr_max(T(0.99), T(1) - mu);
     T dz[NZS];
     for (int i = 0; i < NZS; ++i) dz[i] = T(0);
-#if MR_MFMA_CHAIN
-    fwd_chain<false>(dz);
-#else
     fwd_recursion<false>(dz);
-#endif
 #if MR_PHASE_CYCLES
     const unsigned long long tf1 = trace ? MR_CLOCK() : 0ull;
 #endif
@@ -1889,18 +1482,10 @@ struct WaveSolver {
 #pragma unroll
     for (int r = 0; r <= NROW; ++r) {
       const int j0 = r < NROW ? 2 * r : JL, j1 = j0 + 1;
-#if MR_EVAL_BRANCHFREE
-      // branch-free: an inactive row's operands are replaced by s = lam = 1 and its results selected out
-      // (its step fields written 0; every reader masks them by the row's activity)
-      const bool a = act[j0] != 0;
-      const T t0 = a ? S(sf(cur) + j0) : T(1), t1 = a ? S(sf(cur) + j1) : T(1);
-      const T l0 = a ? S(SSF::LAM + j0) : T(1), l1 = a ? S(SSF::LAM + j1) : T(1);
-#else
       if (!act[j0]) continue;
       const bool a = true;
       const T t0 = S(sf(cur) + j0), t1 = S(sf(cur) + j1);
       const T l0 = S(SSF::LAM + j0), l1 = S(SSF::LAM + j1);
-#endif
       const T s0 = l0 / t0, s1 = l1 / t1;
       T dt0, dt1, dy0, dy1;
       if (r < 2) {
@@ -2178,7 +1763,6 @@ struct WaveSolver {
         T d[NI];
         int act[NI];
         row_values(k, zt, e, d, act);
-#if MR_LS_BRANCHFREE
         if constexpr (!RESTO) {
           // branch-free over the slots (the per-slot activity test compiled to a divergent branch each):
           // an inactive slot has s = 1, ds = 0 (setup above), so s + alpha ds = 1 > 0 and log 1 = 0 add
@@ -2201,9 +1785,8 @@ struct WaveSolver {
             }
           }
         }
-#endif
         for (int j = 0; j < NI; ++j) {
-          if (MR_LS_BRANCHFREE && !RESTO) break;
+          if (!RESTO) break;  // (the regular trial's slots: the branch-free loop above)
           st[j] = s_c[j];
           if (!((actm >> j) & 1u)) {
             if (!RESTO && cap) Cf(CSF::CTR + j) = T(0);
@@ -2275,7 +1858,8 @@ struct WaveSolver {
       if constexpr (RESTO) {
         ph_t = fv - mu * (lg + wsum(w, lgr_l)) + kdm * lin;
         cw()->tho = wsum(w, tho_l);  // the point as the original problem sees it (restoration exit test)
-        cw()->pho = wsum(w, fo_l) - mu_o * lg + T(IP_KAPPA_D) * mu_o * lin;
+        cw()->fo = wsum(w, fo_l);
+        cw()->pho = cw()->fo - mu_o * lg + T(IP_KAPPA_D) * mu_o * lin;
       }
       if (!(th_t == th_t) || !(ph_t == ph_t)) ok = 0;
       return wuni(w, ok != 0);
@@ -2413,27 +1997,6 @@ struct WaveSolver {
       row_values(k, z, e, d, act);
       for (int j = 0; j < NI; ++j)
         Cf(CSF::SR + j) = (act[j] && yslot(j)) ? T(slot_sign(j)) * (d[j] - S(sf(cur) + j)) : T(0);
-#if MR_SOC_GPRE
-      // the costate pass's fixed gradient terms (soc_backward: only SR changes between the tries)
-      const T mu = this->mu, dl = cw()->delta_it;
-      const MR_GLOBAL T* Rk = R(k);
-      for (int i = 0; i < NZ; ++i) Cf(CSF::SGB + i) = Rk[RCF::G0 + i] + mu * Rk[RCF::G1 + i] + dl * Rk[RCF::GD + i];
-#pragma unroll
-      for (int r = 0; r <= NROW; ++r) {
-        const int j0 = r < NROW ? 2 * r : JL, j1 = j0 + 1;
-        T c0 = T(0), c1 = T(0), e0 = T(0), e1 = T(0);
-        if (act[j0]) {
-          const T t0 = S(sf(cur) + j0), t1 = S(sf(cur) + j1);
-          const T s0 = S(SSF::LAM + j0) / t0, s1 = S(SSF::LAM + j1) / t1;
-          e0 = d[j0] - t0;
-          if (r < 2) { c0 = s0 + dl; c1 = s1 + dl; e1 = d[j1] - t1; }
-          else c0 = s0 + s1 + dl;
-        }
-        Cf(CSF::SGR + 4 * r) = c0; Cf(CSF::SGR + 4 * r + 1) = c1;
-        Cf(CSF::SGR + 4 * r + 2) = e0; Cf(CSF::SGR + 4 * r + 3) = e1;
-      }
-      for (int a = 0; a < 3; ++a) Cf(CSF::SGC + a) = e.gC[a];
-#endif
     }
     wsync(w);
   }
@@ -2447,77 +2010,6 @@ struct WaveSolver {
     }
     wsync(w);
   }
-  // The SOC costate recursion on the stored closed-loop map (MR_MFMA_SOCB 3): lane i < NX forms
-  // pv_k[i] = v_k[i] + sum_j Acl_k[j][i] pv_{k+1}[j] -- per stage one broadcast of pv (11 v_readlane) and
-  // an 11-term dot as three chains, its 12 operands (Acl column i, v_k[i]) loaded three stages ahead;
-  // pv_k to LDX row k (LDS only in the loop).  r_k and the feed-forward follow stage-parallel.
-  MR_HD void socb_chain_acl() {
-    const int N = wu(this->w, this->N), ln = this->ln;
-    const Wv w = this->w;
-    const WBuf<T> wb(rc - (int64_t)SSF::NF * WL, (unsigned)WS_NU_OFF);
-    const WBuf<T> mb(mtb(), (unsigned)(NX * NX * WL));
-    const unsigned cold0 = (unsigned)(SSF::NF * WL) + (unsigned)RC_STRIDE * WL;
-    MR_LDS T* const LDX = lds + LDX_OFF;
-    const bool row = ln < NX;
-    const int li = row ? ln : 0;
-    const unsigned voff = (unsigned)(CSF::SPV + li) * WL;
-    unsigned moff[NX];
-#pragma unroll
-    for (int j = 0; j < NX; ++j) moff[j] = (unsigned)(li * NX + j) * WL;
-    // LDS target: row k of LDX for lanes < NX, the lane's discard slot otherwise (address = base + k stride)
-    const int lbase = row ? LDX_OFF + ln : LJUNK_OFF + ln, lstride = row ? 12 : 0;
-    struct Ops {
-      T m[NX], v;
-    };
-    auto ld = [&](int k, Ops& o) {
-      const unsigned ku = (unsigned)wu(w, k), ck = (unsigned)wu(w, (int)(cold0 + (unsigned)k));
-#pragma unroll
-      for (int j = 0; j < NX; ++j) o.m[j] = mb.ld(ku, moff[j]);
-      o.v = wb.ld(ck, voff);
-    };
-    T pv = wb.ld((unsigned)wu(w, (int)(cold0 + (unsigned)N)), (unsigned)(CSF::SG + li) * WL);  // pv_N = g_x,N
-    lds[lbase + lstride * N] = pv;
-    auto step = [&](int k, const Ops& o) {
-      T p[NX];
-      wgather<T, NX>(w, pv, p);
-      T a0 = o.v + o.m[0] * p[0], a1 = o.m[1] * p[1], a2 = o.m[2] * p[2];
-#pragma unroll
-      for (int j = 3; j < NX; j += 3) {
-        a0 += o.m[j] * p[j];
-        if (j + 1 < NX) a1 += o.m[j + 1] * p[j + 1];
-        if (j + 2 < NX) a2 += o.m[j + 2] * p[j + 2];
-      }
-      pv = (a0 + a1) + a2;
-      lds[lbase + lstride * k] = pv;
-    };
-    if (N > 0) {
-      auto kc = [](int k) { return k > 0 ? k : 0; };
-      Ops b0, b1, b2, b3;
-      ld(N - 1, b0);
-      ld(kc(N - 2), b1);
-      ld(kc(N - 3), b2);
-      for (int k = N - 1;; k -= 4) {
-        ld(kc(k - 3), b3);
-        MR_SCHED_BARRIER();
-        step(k, b0);
-        if (k == 0) break;
-        ld(kc(k - 4), b0);
-        MR_SCHED_BARRIER();
-        step(k - 1, b1);
-        if (k == 1) break;
-        ld(kc(k - 5), b1);
-        MR_SCHED_BARRIER();
-        step(k - 2, b2);
-        if (k == 2) break;
-        ld(kc(k - 6), b2);
-        MR_SCHED_BARRIER();
-        step(k - 3, b3);
-        if (k == 3) break;
-      }
-    }
-    wsync_lds(w);
-  }
-
   // The SOC costate recursion given v_k, u_k (cold fields SPV, SK0: everything that does not depend on
   // pv_{k+1}): lane i < NX forms pv_k[i] = v_k[i] + (A_k^T pv_{k+1})[i] + sum_a K_k[a][i] (B_k^T pv_{k+1})[a]
   // from pv_{k+1} broadcast by v_readlane; B_k^T pv_{k+1} (the same in every lane) plus u_k is r_k, the
@@ -2640,32 +2132,6 @@ struct WaveSolver {
 #endif
     const T mu = this->mu, dl = cw()->delta_it;
     const int N = wu(w, this->N);
-#if MR_SOC_GPRE
-    (void)mu; (void)dl;
-    if (own()) {  // g from soc_prepare's fixed terms and this try's SR (same arithmetic as below)
-      T g[NZ];
-      for (int i = 0; i < NZ; ++i) g[i] = Cf(CSF::SGB + i);
-#pragma unroll
-      for (int r = 0; r <= NROW; ++r) {
-        const int j0 = r < NROW ? 2 * r : JL, j1 = j0 + 1;
-        const T c0 = Cf(CSF::SGR + 4 * r), c1 = Cf(CSF::SGR + 4 * r + 1);
-        const T e0 = Cf(CSF::SGR + 4 * r + 2), e1 = Cf(CSF::SGR + 4 * r + 3);
-        if (c0 == T(0) && c1 == T(0)) continue;  // inactive row (an active row's c0 = lam / s + delta > 0)
-        T dg;
-        if (r < 2) dg = c0 * (Cf(CSF::SR + j0) - e0) + c1 * (Cf(CSF::SR + j1) + e1);
-        else dg = c0 * (Cf(CSF::SR + j0) - e0);
-        if (r < NROW) {
-#pragma unroll
-          for (int a = 0; a < RN(r); ++a) g[RI(r, a)] += T(RS(a)) * dg;
-        } else {
-          g[0] += Cf(CSF::SGC + 0) * dg;
-          g[1] += Cf(CSF::SGC + 1) * dg;
-          g[6] += Cf(CSF::SGC + 2) * dg;
-        }
-      }
-      for (int i = 0; i < NZ; ++i) Cf(CSF::SG + i) = g[i];
-    }
-#else
     if (own()) {
       const int k = ln;
       const MR_GLOBAL T* Rk = R(k);
@@ -2698,15 +2164,12 @@ struct WaveSolver {
       }
       for (int i = 0; i < NZ; ++i) Cf(CSF::SG + i) = g[i];
     }
-#endif
     wsync(w);
     MR_TSUB(12);
-#if MR_MFMA_SOCB
     // pv_k = Acl_k^T pv_{k+1} + v_k with v_k = A_k^T q + K_k^T u_k + g_x, q = P_{k+1} c_k, u_k = B_k^T q + g_u
     // (then r_k = B_k^T pv_{k+1} + u_k): v_k, u_k stage-parallel into the cold fields SPV / SK0 (everything
-    // that does not depend on pv_{k+1}), then the recursion -- MR_MFMA_SOCB 1: mfma_chain<TR>; 2: a lean
-    // lane recursion (socb_chain: pv_{k+1} broadcast, A_k^T pv + K_k^T (B_k^T pv) + v_k, r_k on the way) --
-    // then the feed-forward stage-parallel
+    // that does not depend on pv_{k+1}), then the lean lane recursion (socb_chain: pv_{k+1} broadcast,
+    // A_k^T pv + K_k^T (B_k^T pv) + v_k, r_k on the way), then the feed-forward stage-parallel
     if (own() && ln < N) {
       const int k = ln;
       const MR_GLOBAL T* Rk = R(k);
@@ -2731,51 +2194,8 @@ struct WaveSolver {
         Cf(CSF::SPV + r) = v;
       }
       for (int a = 0; a < NU; ++a) Cf(CSF::SK0 + a) = u[a];
-#if MR_MFMA_SOCB == 3
-      // Acl_k = A_k + B_k K_k (mr_solver.h apply_A / apply_B's structure), column i to fields i NX + j
-      MR_GLOBAL T* const mt = mtb();
-      for (int i = 0; i < NX; ++i) {
-        for (int j = 0; j < 6; ++j) {
-          const T a = i < 6 ? J[j * 8 + i] : T(0);
-          mt[(i * NX + j) * WL + k] = a + J[j * 8 + 6] * Kr[0][i] + J[j * 8 + 7] * Kr[1][i];
-        }
-        mt[(i * NX + 6) * WL + k] = (i == 6 ? T(1) : T(0)) + Kr[2][i];
-        mt[(i * NX + 7) * WL + k] = Kr[0][i];
-        mt[(i * NX + 8) * WL + k] = Kr[1][i];
-        mt[(i * NX + 9) * WL + k] = k > 0 ? (i == 9 ? T(1) : T(0)) : Kr[0][i];
-        mt[(i * NX + 10) * WL + k] = k > 0 ? (i == 10 ? T(1) : T(0)) : Kr[1][i];
-      }
-#endif
     }
     MR_LDS T* const LDX = lds + LDX_OFF;
-#if MR_MFMA_SOCB == 3
-    wsync(w);  // v_k, u_k (cold fields) and Acl visible
-    MR_TSUB(13);
-    socb_chain_acl();
-    MR_TSUB(14);
-    if (own()) {  // r_k = B_k^T pv_{k+1} + u_k, k_k = -Q_uu^-1 r_k; pv_k to SPV
-      const int k = ln;
-      T pv[NX];
-      for (int r = 0; r < NX; ++r) pv[r] = LDX[k * 12 + r];
-      if (k < N) {
-        const MR_GLOBAL T* Rk = R(k);
-        T pn[NX];
-        for (int r = 0; r < NX; ++r) pn[r] = LDX[(k + 1) * 12 + r];
-        T r0 = pn[7], r1 = pn[8];
-        if (k == 0) { r0 += pn[9]; r1 += pn[10]; }
-        for (int j = 0; j < 6; ++j) { r0 += Rk[RCF::J + j * 8 + 6] * pn[j]; r1 += Rk[RCF::J + j * 8 + 7] * pn[j]; }
-        const T Lf[6] = {T(0), Rk[RCF::LQ + 0], T(0), Rk[RCF::LQ + 1], Rk[RCF::LQ + 2], T(0)};
-        const T iv[3] = {Rk[RCF::LQ + 3], Rk[RCF::LQ + 4], Rk[RCF::LQ + 5]};
-        T kf[NU] = {-(r0 + Cf(CSF::SK0 + 0)), -(r1 + Cf(CSF::SK0 + 1)), -(pn[6] + Cf(CSF::SK0 + 2))};
-        lsolve3r(Lf, iv, kf);
-        ltsolve3r(Lf, iv, kf);
-        for (int a = 0; a < NU; ++a) Cf(CSF::SK0 + a) = kf[a];
-      }
-      for (int r = 0; r < NX; ++r) Cf(CSF::SPV + r) = pv[r];
-    }
-    wsync(w);
-    MR_TSUB(15);
-#elif MR_MFMA_SOCB == 2
     wsync(w);  // v_k, u_k (cold fields) visible
     MR_TSUB(13);
     socb_chain();
@@ -2798,131 +2218,6 @@ struct WaveSolver {
     }
     wsync(w);
     MR_TSUB(15);
-#else
-    {  // pv_N = g_x,N: the chain's start (B operand rows 4s + g) and LDX row N
-      const int g = ln >> 4;
-      const MR_GLOBAL T* cbN = rc + (int64_t)RC_STRIDE * WL + N;
-      T y0[3];
-      for (int s2 = 0; s2 < 3; ++s2) {
-        const int r = 4 * s2 + g;
-        y0[s2] = r < NX ? cbN[(CSF::SG + (r < NX ? r : 0)) * WL] : (r == 11 ? T(1) : T(0));
-      }
-      if (ln < NX) LDX[N * 12 + ln] = cbN[(CSF::SG + ln) * WL];
-      wsync(w);  // v_k, u_k (cold fields) and row N visible
-      mfma_chain<true, false>(y0);
-    }
-    if (own()) {
-      const int k = ln;
-      T pv[NX];
-      for (int r = 0; r < NX; ++r) pv[r] = LDX[k * 12 + r];
-      if (k < N) {
-        const MR_GLOBAL T* Rk = R(k);
-        T J[48], pn[NX], r3[NU];
-        for (int j = 0; j < 48; ++j) J[j] = Rk[RCF::J + j];
-        for (int r = 0; r < NX; ++r) pn[r] = LDX[(k + 1) * 12 + r];
-        apply_Bt(J, k, pn, r3);
-        const T Lf[6] = {T(0), Rk[RCF::LQ + 0], T(0), Rk[RCF::LQ + 1], Rk[RCF::LQ + 2], T(0)};
-        const T iv[3] = {Rk[RCF::LQ + 3], Rk[RCF::LQ + 4], Rk[RCF::LQ + 5]};
-        T kf[NU];
-        for (int a = 0; a < NU; ++a) kf[a] = -(r3[a] + Cf(CSF::SK0 + a));
-        lsolve3r(Lf, iv, kf);
-        ltsolve3r(Lf, iv, kf);
-        for (int a = 0; a < NU; ++a) Cf(CSF::SK0 + a) = kf[a];
-      }
-      for (int r = 0; r < NX; ++r) Cf(CSF::SPV + r) = pv[r];
-    }
-    wsync(w);
-#endif
-#else
-    const MR_GLOBAL T* cb = rc + (int64_t)RC_STRIDE * WL;
-    const WBuf<T> wb(rc + (int64_t)RC_STRIDE * WL, (unsigned)CSF::NF * WL);
-    const bool row = ln < NX;
-    const int li = row ? ln : 0;
-    const unsigned junk = (unsigned)(CSF::SJUNK * WL + ln);
-    // one stage's operands: P_{k+1} row li, c_k, A_k column li (J column li, vehicle rows), B's J
-    // columns, K_k column li, Q_uu's factor, g_x[li], g_u
-    // the shared operands (c_k, B's J columns, Q_uu's factor, g_u) are loaded one word per lane and
-    // broadcast by v_readlane at use: one vector load each instead of one per word
-    const int l12 = ln < 12 ? ln : 0;
-    struct Ops {
-      T prow[NX], acol[6], kcol[NU], gx, c_w, jb_w, gu_w;
-    };
-    auto ld = [&](int k, Ops& o) {
-      const MR_GLOBAL T* Rk = R(k);
-      const MR_GLOBAL T* Rn = R(k + 1);
-      for (int l = 0; l < NX; ++l) o.prow[l] = Rn[RCF::P + pidx(li, l)];
-      for (int j = 0; j < 6; ++j) o.acol[j] = Rk[RCF::J + j * 8 + (li < 6 ? li : 0)];
-      for (int a = 0; a < NU; ++a) o.kcol[a] = Rk[RCF::K + a * NX + li];
-      o.gx = cb[(CSF::SG + li) * WL + k];
-      o.c_w = cb[(CSF::SC + li) * WL + k];                        // lane l: c_k[l]
-      o.jb_w = Rk[RCF::J + (l12 >> 1) * 8 + 6 + (l12 & 1)];      // lane 2j + a: J[j][6 + a]
-      o.gu_w = cb[(CSF::SG + NX + (ln < NU ? ln : 0)) * WL + k];  // lane a: g_u[a]
-    };
-    T pv = cb[(CSF::SG + li) * WL + N];
-    wb.st(pv, 0u, row ? (unsigned)((CSF::SPV + li) * WL + N) : junk);
-    auto step = [&](int k, const Ops& o) {
-      T c[NX], jb[12], gu[NU];
-      wgather<T, NX>(w, o.c_w, c);
-      wgather<T, 12>(w, o.jb_w, jb);
-      wgather<T, NU>(w, o.gu_w, gu);
-      T pcl = pv;
-      for (int l = 0; l < NX; ++l) pcl += o.prow[l] * c[l];
-      T pc[NX];
-      wgather<T, NX>(w, pcl, pc);
-      // r = B^T pc + g_u (mr_solver.h apply_Bt), every lane
-      T r[NU] = {pc[7] + gu[0], pc[8] + gu[1], pc[6] + gu[2]};
-      if (k == 0) { r[0] += pc[9]; r[1] += pc[10]; }
-      for (int j = 0; j < 6; ++j) { r[0] += jb[2 * j] * pc[j]; r[1] += jb[2 * j + 1] * pc[j]; }
-      // (A^T pc)[li] (mr_solver.h apply_At)
-      T at;
-      if (li < 6) {
-        at = T(0);
-        for (int j = 0; j < 6; ++j) at += o.acol[j] * pc[j];
-      } else {
-        at = li == 6 ? pc[6] : ((li >= 9 && k > 0) ? (li == 9 ? pc[9] : pc[10]) : T(0));
-      }
-      pv = o.gx + at + o.kcol[0] * r[0] + o.kcol[1] * r[1] + o.kcol[2] * r[2];
-      wb.st(pv, 0u, row ? (unsigned)((CSF::SPV + li) * WL + k) : junk);
-      // r to SK0 (lanes 0..2); the feed-forward k_k = -Q_uu^-1 r is formed stage-parallel afterwards
-      const T rv = ln == 0 ? r[0] : (ln == 1 ? r[1] : r[2]);
-      wb.st(rv, 0u, ln < NU ? (unsigned)((CSF::SK0 + ln) * WL + k) : junk);
-    };
-    // operands three stages ahead, four rotating sets (unrolled by four: compile-time set roles, no
-    // register copies of in-flight loads; one stage ahead left every stage waiting out a memory round
-    // trip); a prefetch past stage 0 re-reads stage 0 (unconditional loads, exact waits)
-    if (N > 0) {
-      auto kc = [](int k) { return k > 0 ? k : 0; };
-      Ops b0, b1, b2, b3;
-      ld(N - 1, b0);
-      ld(kc(N - 2), b1);
-      ld(kc(N - 3), b2);
-      for (int k = N - 1;; k -= 4) {
-        ld(kc(k - 3), b3);
-        step(k, b0);
-        if (k == 0) break;
-        ld(kc(k - 4), b0);
-        step(k - 1, b1);
-        if (k == 1) break;
-        ld(kc(k - 5), b1);
-        step(k - 2, b2);
-        if (k == 2) break;
-        ld(kc(k - 6), b2);
-        step(k - 3, b3);
-        if (k == 3) break;
-      }
-    }
-    wsync(w);
-    if (own() && ln < N) {  // k_k = -Q_uu^-1 r (L10, L20, L21 and the reciprocal pivots from the Riccati sweep)
-      const MR_GLOBAL T* Rk = R(ln);
-      const T Lf[6] = {T(0), Rk[RCF::LQ + 0], T(0), Rk[RCF::LQ + 1], Rk[RCF::LQ + 2], T(0)};
-      const T iv[3] = {Rk[RCF::LQ + 3], Rk[RCF::LQ + 4], Rk[RCF::LQ + 5]};
-      T kf[NU] = {-Cf(CSF::SK0 + 0), -Cf(CSF::SK0 + 1), -Cf(CSF::SK0 + 2)};
-      lsolve3r(Lf, iv, kf);
-      ltsolve3r(Lf, iv, kf);
-      for (int a = 0; a < NU; ++a) Cf(CSF::SK0 + a) = kf[a];
-    }
-    wsync(w);
-#endif
 #undef MR_TSUB
   }
   // the SOC direction (mr_solver.h Solver::forward with soc set): SDZ, SDS, SDLAM, SDY, SDNU.  The recursion
@@ -2938,11 +2233,7 @@ struct WaveSolver {
 #if MR_PHASE_CYCLES
     const unsigned long long tc0 = trace ? MR_CLOCK() : 0ull;
 #endif
-#if MR_MFMA_CHAIN
-    fwd_chain<true>(dzr);
-#else
     fwd_recursion<true>(dzr);
-#endif
     wsync(w);  // SDNU (the recursion's costate steps) visible
 #if MR_PHASE_CYCLES
     if (trace) tsub[2] += MR_CLOCK() - tc0;
@@ -3105,7 +2396,7 @@ struct WaveSolver {
     T znext[NX], c[NX], d[NI];
     int act[NI];
     for (int i = 0; i < NX; ++i) { znext[i] = wnext(w, z[i]); c[i] = T(0); }
-    T pr_l = T(0), th_def_l = T(0);
+    T pr_l = T(0), th_def_l = T(0), fo_l = T(0);
     if (own()) {
       if (k < N) {
         T xn[NX];
@@ -3121,7 +2412,10 @@ struct WaveSolver {
       row_values(k, z, e, d, act);
       for (int j = 0; j < NI; ++j)
         if (act[j] && yslot(j)) pr_l = mr_max(pr_l, mr_abs(d[j] - S(sf(cur) + j)));
+      fo_l = stage_cost(P, I, k, z, e, sc, (T*)nullptr, (T*)nullptr);
     }
+    // the original objective at the entry point (reported if the restoration phase ends the solve)
+    C->fo_cur = wsum(w, fo_l);
     // IPOPT's RestoIterateInitializer: mu_r = max(mu, ||c||_inf, ||d - s||_inf)
     const T mu_r = mr_max(mu, wmax(w, pr_l));
     const T th_r = wsum(w, th_def_l);  // relaxed rows start satisfied: the definitional rows only
@@ -3477,11 +2771,6 @@ struct WaveSolver {
 #define MR_STAT(x) ((void)0)
 #endif
     for (it = 0;; ++it) {
-#if MR_DEVICE_BUILD && MR_PRIO_ITER > 0
-      // long solves: raise the wave's issue priority over the partner wave on its SIMD, so the
-      // batch's slowest instances (which set its makespan) are not slowed by the short ones
-      if (it == MR_PRIO_ITER) __builtin_amdgcn_s_setprio(3);
-#endif
       // wave-uniform mode of this iteration: the original problem, or its restoration phase
       const bool rs = wuni(w, cw()->resto != 0);
       MR_T0();
@@ -3600,8 +2889,9 @@ struct WaveSolver {
         MR_T1(3);
         MR_STAT((st_resto++, st_trials += res_ntr));
         if (!(res_flags & LSR_ACC)) { out.status = 3; break; }  // IPOPT: restoration failed
+        cw()->fo_cur = cw()->fo;  // the accepted step's point is the last trial evaluated (no SOC here)
         if (res_flags & LSR_AUG) filter_add((T(1) - g_th) * th, ph - g_ph * th);
-        if (trace && ln == 0 && it < trace_cap - 2) {
+        if (trace && ln == 0 && it < trace_cap - MR_TRACE_RESERVED) {
           double* tr = trace + 8 * it;
           tr[0] = (double)kkt; tr[1] = (double)mu; tr[2] = (double)res_alpha; tr[3] = (double)ad;
           tr[4] = (double)delta; tr[5] = (double)th; tr[6] = (double)cw()->tho; tr[7] = -200.0 - res_nls;
@@ -3697,7 +2987,7 @@ struct WaveSolver {
             accepted = (flags & LSR_ACC) != 0;
           }
         } else {
-          line_search<false, false>(th, ph, gphi, th_pow, ap, ap, a_min, 0, MR_SOC_CAPTURE ? LS_CAP : 0, T(0), T(-1));
+          line_search<false, false>(th, ph, gphi, th_pow, ap, ap, a_min, 0, LS_CAP, T(0), T(-1));
           flags = res_flags;
           rejf |= (flags & LSR_REJF) != 0;
           accepted = (flags & LSR_ACC) != 0;
@@ -3711,13 +3001,8 @@ struct WaveSolver {
               if (count > 0 && !(th_trial <= T(IP_KAPPA_SOC) * th_old)) break;
               th_old = th_trial;
               // the trial point's constraint values: captured by its own evaluation (the first trial of the
-              // line search, or the previous correction's trial), else evaluated again
-              if (MR_SOC_CAPTURE)
-                soc_accumulate(a_soc);
-              else if (count == 0)
-                line_search<false, false>(th, ph, gphi, th_pow, a_soc, ap, a_min, 0, LS_ACC, a_soc, a_soc);
-              else
-                line_search<false, true>(th, ph, gphi, th_pow, a_soc, ap, a_min, 0, LS_ACC, a_soc, a_soc);
+              // line search, or the previous correction's trial)
+              soc_accumulate(a_soc);
               MR_STAT(st_soc_try++);
               MR_CNT(5);
 #if MR_PHASE_CYCLES
@@ -3732,7 +3017,7 @@ struct WaveSolver {
 #if MR_PHASE_CYCLES
               if (trace) { tsub[6] += ts1 - ts0; tsub[7] += MR_CLOCK() - ts1; }
 #endif
-              line_search<false, true>(th, ph, gphi, th_pow, aps, aps, aps, 0, MR_SOC_CAPTURE ? (LS_WD | LS_CAP) : LS_WD,
+              line_search<false, true>(th, ph, gphi, th_pow, aps, aps, aps, 0, LS_WD | LS_CAP,
                                        a_test0, T(-1));
               rejf |= (res_flags & LSR_REJF) != 0;
               a_soc = aps;
@@ -3794,7 +3079,7 @@ struct WaveSolver {
         cw()->in_wd = 0;
         cw()->wd_short = 0;
         acc_count = 0;
-        if (trace && ln == 0 && it < trace_cap - 2) {
+        if (trace && ln == 0 && it < trace_cap - MR_TRACE_RESERVED) {
           double* tr = trace + 8 * it;
           tr[0] = (double)kkt; tr[1] = (double)mu; tr[2] = 0.0; tr[3] = 0.0;
           tr[4] = (double)delta; tr[5] = (double)th; tr[6] = (double)ph; tr[7] = -300.0;
@@ -3817,7 +3102,7 @@ struct WaveSolver {
       if (!take_anyway && (soft_step ? soft_orig : (!tiny && (flags & LSR_AUG))))
         filter_add((T(1) - g_th) * uth, uph - g_ph * uth);
       if (soft_step) ad = alpha;  // the soft restoration step moves every variable by one step size
-      if (trace && ln == 0 && it < trace_cap - 2) {
+      if (trace && ln == 0 && it < trace_cap - MR_TRACE_RESERVED) {
         double* tr = trace + 8 * it;
         tr[0] = (double)kkt; tr[1] = (double)mu; tr[2] = (double)alpha; tr[3] = (double)ad;
         tr[4] = (double)delta; tr[5] = (double)uth; tr[6] = (double)uph;
@@ -3830,6 +3115,10 @@ struct WaveSolver {
       wsync(w);  // new iterate buffer written by every lane before the next evaluation
     }
     out.iters = it;
+    // a solve that ends inside the restoration phase returns the restoration iterate: its objective is the
+    // original problem's there (the restoration NLP's own objective is rho |p + n| + proximity), its
+    // constraint violation out.viol was set as the original problem's at the loop top
+    if (wuni(w, cw()->resto != 0)) out.obj = (double)(cw()->fo_cur / sc);
 #ifdef MR_WAVE_STATS
     if (ln == 0)
       printf("wave stats: status %d iters %d trials %ld soc_try %ld soc_ok %ld resto %ld wd %ld fact %ld lsfail %ld\n",
@@ -3852,7 +3141,7 @@ struct WaveSolver {
       }
     }
 #endif
-    if (trace && ln == 0 && it < trace_cap - 2) {
+    if (trace && ln == 0 && it < trace_cap - MR_TRACE_RESERVED) {
       double* tr = trace + 8 * it;
       tr[0] = (double)out.kkt; tr[1] = (double)fval; tr[2] = (double)theta; tr[3] = (double)stat_max;
       tr[4] = (double)pr_max; tr[5] = (double)sc; tr[6] = (double)mu; tr[7] = 1000.0 + out.status;

@@ -5,10 +5,6 @@ bounds of mpcracing.hip): variants/lib_<name>.so, run by tools/gpu_flags_ab.sh o
   denorm   fp32 denormals kept (no -fgpu-flush-denormals-to-zero)
   slp      SLP vectorisation on (no -fno-slp-vectorize)
   w1       fp32 solve kernel at 1 wave per SIMD (MR_WAVES_PER_SIMD_F32=1, 512 VGPRs)
-  ric3     Riccati operand gathers three stages ahead instead of two (MR_RIC_AHEAD=3)
-  s464     a 464-word record stride (the footprint the rejected paired factorisation needed, git e417017)
-  s336     the 336-word record stride of the build that still stored p1 / k1 (git 60d581f)
-  prio60   waves past iteration 60 raise their issue priority (s_setprio 3)
   cyc      per-sweep shader-cycle counters of the trace instance (tools/phase_probe.py)
 """
 import os
@@ -25,10 +21,6 @@ VARIANTS = {
     "denorm": [f for f in DEFAULT_FLAGS if f != "-fgpu-flush-denormals-to-zero"],
     "slp": [f for f in DEFAULT_FLAGS if f != "-fno-slp-vectorize"],
     "w1": DEFAULT_FLAGS + ["-DMR_WAVES_PER_SIMD_F32=1"],
-    "ric3": DEFAULT_FLAGS + ["-DMR_RIC_AHEAD=3"],
-    "s464": DEFAULT_FLAGS + ["-DMR_RC_STRIDE_FORCE=464"],
-    "s336": DEFAULT_FLAGS + ["-DMR_RC_STRIDE_FORCE=336"],
-    "prio60": DEFAULT_FLAGS + ["-DMR_PRIO_ITER=60"],
     "cyc": DEFAULT_FLAGS + ["-DMR_PHASE_CYCLES=1"],
 }
 

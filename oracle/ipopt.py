@@ -130,10 +130,13 @@ class Rules:
 
 
 IPOPT = Rules()
-# the rules of the product (csrc/mr_solver.h, csrc/mr_wave.h): IPOPT's, with the restoration phase's documented
-# simplifications; the restoration phase's own iterates are not compared (the product also keeps
-# X_0 / S_0 hard and relaxes a two-sided row's distances separately)
-PRODUCT = replace(IPOPT, resto_ls_mult=False, resto_soc=False, resto_watchdog=False, resto_relax_x0=False)
+# the rules of the product (csrc/mr_solver.h, csrc/mr_wave.h): IPOPT's, less the tiny-step termination (compiled
+# out, MR_TINY_STEP 0: it reads the step's rounding floor) and with the restoration phase's
+# documented simplifications; the restoration phase's own iterates are not compared (the product also relaxes a
+# two-sided row's distances separately).  Every field here must mirror a compile-time rule of the kernel:
+# tests/test_rules_label.py reads them back from mr_solver.h.
+PRODUCT = replace(IPOPT, tiny_step=False, resto_ls_mult=False, resto_soc=False, resto_watchdog=False,
+                  resto_relax_x0=False)
 R3 = Rules(opti_rows=False, bound_relax_factor=0.0, constr_scaling=False, ls_mult_init=False, separate_yd=False,
            sd_count_yd=False, kappa_d=0.0, delta_s=False, delta_inc_1e5=False, unscaled_tests=False, mu_floor="tol10",
            nlp_error_viol=False, max_soc=-1, ftype_rule="r3", first_trial=False, obj_max_inc=0.0, compare_eps=False,

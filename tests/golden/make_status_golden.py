@@ -19,7 +19,13 @@ Parity note: this pins the product against the RESTATEMENT of IPOPT's published 
 itself the status class stays unpinned (no IPOPT / CasADi in this image, none of its output in the
 reference).
 
-Usage: python tests/golden/make_status_golden.py [C1dyn C1kin C2 C4 C5]   (--procs 8)
+Second column (--rules=PRODUCT, keys prefixed PRODUCT_): the same instances under the product's rule set
+(``ipopt.PRODUCT``: IPOPT's without the tiny-step termination, whose trigger -- every step component below
+10 eps of double relative -- reads the linear solver's rounding floor at the mu floor).  The
+product's statuses are held to this column on every instance; against the IPOPT column they differ only
+where IPOPT's rounding-floor test fires, and there the returned point is the same (tests/test_status_golden.py).
+
+Usage: python tests/golden/make_status_golden.py [C1dyn C1kin C2 C4 C5]   (--procs=8) (--rules=IPOPT|PRODUCT)
 """
 import json
 import os
@@ -64,8 +70,8 @@ def _solve(args):
     torch.set_num_threads(1)
     from mpcracing import workload as wl
     from oracle.nlp import MPCProblem
-    from oracle.ipopt import IPOPT, solve_ipopt
-    name, i = args
+    from oracle import ipopt
+    name, i, rn = args
     cfg, b = _config(name)
     tyres = wl.tyre_coeffs(cfg["tyres"]) if cfg["tyres"] else None
     j = sample_indices(name)[i]
@@ -73,7 +79,7 @@ def _solve(args):
     p = MPCProblem(inst["state0"], inst["s0"], inst["cx"], inst["cy"], inst["max_error"], N=cfg["N"], Ts=cfg["Ts"],
                    model=cfg["model"], lane_bounds=cfg["lane"], tyres=tyres)
     t0 = time.time()
-    r = solve_ipopt(p, rules=IPOPT, **OPTIONS)
+    r = ipopt.solve_ipopt(p, rules=getattr(ipopt, rn), **OPTIONS)
     X, U, S, eC, eL = p.unpack(r.w)
     w = torch.tensor(r.w, dtype=torch.float64)
     d, dL, dU, _k = p.ipopt_ineq()
@@ -88,24 +94,26 @@ def _solve(args):
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     procs = int(next((a.split("=")[1] for a in sys.argv[1:] if a.startswith("--procs=")), 8))
+    rn = next((a.split("=")[1] for a in sys.argv[1:] if a.startswith("--rules=")), "IPOPT")
+    pre = "" if rn == "IPOPT" else rn + "_"
     names = args or ["C1dyn", "C1kin", "C2", "C4", "C5"]
-    jobs = [(n, i) for n in names for i in range(_n(n))]
+    jobs = [(n, i, rn) for n in names for i in range(_n(n))]
     with Pool(procs) as pool:
         res = pool.map(_solve, jobs, chunksize=1)
     out = dict(np.load(OUT)) if os.path.exists(OUT) else {}
     for name in names:
-        rs = sorted([r for (n, _), r in zip(jobs, res) if n == name], key=lambda r: r["i"])
+        rs = sorted([r for (n, _i, _r), r in zip(jobs, res) if n == name], key=lambda r: r["i"])
         for k in ("X", "U", "S"):
-            out[f"{name}_{k}"] = np.stack([r[k] for r in rs], axis=-1)
+            out[f"{pre}{name}_{k}"] = np.stack([r[k] for r in rs], axis=-1)
         for k in ("status", "iters"):
-            out[f"{name}_{k}"] = np.array([r[k] for r in rs], dtype=np.int32)
+            out[f"{pre}{name}_{k}"] = np.array([r[k] for r in rs], dtype=np.int32)
         for k in ("obj", "kkt", "viol"):
-            out[f"{name}_{k}"] = np.array([r[k] for r in rs])
-        out[f"{name}_why"] = np.array([r["why"] for r in rs])
+            out[f"{pre}{name}_{k}"] = np.array([r[k] for r in rs])
+        out[f"{pre}{name}_why"] = np.array([r["why"] for r in rs])
         out[f"{name}_idx"] = np.array(sample_indices(name), dtype=np.int64)
-        summ = {"config": name, "n": _n(name), "options": OPTIONS, "rules": "IPOPT",
-                "status_counts": np.bincount(out[f"{name}_status"], minlength=5).tolist(),
-                "status": out[f"{name}_status"].tolist(), "iters": out[f"{name}_iters"].tolist(),
+        summ = {"config": name, "n": _n(name), "options": OPTIONS, "rules": rn,
+                "status_counts": np.bincount(out[f"{pre}{name}_status"], minlength=5).tolist(),
+                "status": out[f"{pre}{name}_status"].tolist(), "iters": out[f"{pre}{name}_iters"].tolist(),
                 "why": [r["why"] for r in rs], "seconds": round(sum(r["t"] for r in rs), 1),
                 "stats_total": {k: int(sum(r["stats"][k] for r in rs)) for k in rs[0]["stats"]}}
         print(json.dumps(summ), flush=True)

@@ -255,6 +255,9 @@ def test_abi_errors():
     ndev = torch.cuda.device_count()
     with pytest.raises(RuntimeError, match="out of range"):
         BatchSolver(20, "kin", max_batch=1, device=ndev)
+    # max_iter beyond the line-search filter's capacity (mr_solver.h FCAP) is rejected, not silently truncated
+    with pytest.raises(RuntimeError, match="max_iter out of range"):
+        BatchSolver(20, "kin", max_batch=1, max_iter=10000)
     import ctypes
     from mpcracing import abi
     lib = abi.load_product()

@@ -240,3 +240,37 @@ def test_second_order_corrections_wave_matches_scalar():
     assert (ta[:, 7] >= 100).sum() >= 5  # corrections accepted
     np.testing.assert_array_equal(ta[:, 7], tw[:, 7])
     np.testing.assert_allclose(tw[:, :7], ta[:, :7], rtol=1e-6, atol=1e-12)
+
+
+def test_max_iter_beyond_filter_capacity_rejected():
+    """A max_iter the line-search filter cannot hold (mr_solver.h FCAP) is an error of the solve call (the GPU
+    library's mr_create rejects it too, test_gpu.py::test_abi_errors), not a silent loss of filter entries."""
+    b = wl.make_batch("C2", limit=1)
+    for scalar in (False, True):
+        with pytest.raises(AssertionError):
+            ht.solve(ht.config(20, "kin", max_iter=10000), b, nthreads=1, scalar=scalar)
+
+
+def test_restoration_exit_reports_the_restoration_iterate_objective():
+    """A solve that ends inside the restoration phase (C3 instance 706 of tests/golden/c3_sample_ipopt.npz, IPOPT's
+    local infeasibility there) returns the restoration iterate; its reported objective is the reference's
+    objective (control/MPC.py:84-98) at exactly that returned point, not the last regular iteration's."""
+    from oracle.nlp import MPCProblem
+    import torch
+    cfg = wl.CONFIGS["C3"]
+    i = 706
+    b = wl.make_batch("C3", limit=i + 1)
+    sub = {k: (v[..., i:i + 1].copy() if v is not None else None) for k, v in b.items()}
+    for scalar in (False, True):
+        o = ht.solve(ht.config(cfg["N"], cfg["model"], "fp64", cfg["lane"], cfg["Ts"], tol=1e-8, acceptable_tol=1e-6,
+                               acceptable_iter=15), sub, nthreads=1, scalar=scalar, trace_instance=0, trace_cap=520)
+        # the emulated wave ends with IPOPT's local infeasibility (4), the scalar build with restoration failure
+        # (3); both inside the restoration phase (trace code <= -200: a restoration iteration)
+        it = o["iters"][0]
+        assert o["status"][0] in (3, 4) and o["trace"][it - 1, 7] <= -200, (o["status"], o["trace"][it - 1])
+        inst = wl.instance_dicts(b)[i]
+        p = MPCProblem(inst["state0"], inst["s0"], inst["cx"], inst["cy"], inst["max_error"], N=cfg["N"],
+                       Ts=cfg["Ts"], model=cfg["model"], lane_bounds=cfg["lane"])
+        w = np.concatenate([o["U"][:, :, 0].ravel(), o["S"][:, 0], o["X"][:, :, 0].ravel()])
+        f = float(p.f(torch.tensor(w)))
+        np.testing.assert_allclose(o["obj"][0], f, rtol=1e-9, atol=1e-9)
