@@ -510,6 +510,9 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "mr_wave_kernel", "avg_launch_ms": kavg * 1e3,
                          "alg_bytes_per_launch": alg_bytes,
+                         "scope": ("per rank: rank 0's algorithmic bytes per launch over rank 0's average launch "
+                                   "time (weak scaling: every rank solves an equal shard; the whole job's "
+                                   "throughput is `value`)") if world > 1 else "the single GPU's launch",
                          "copy_gbs": copy_gbs,
                          "frac_vs_copy": (achieved / copy_gbs) if copy_gbs else None,
                          "copy_source": "measured in this run: 1 GiB fp32 device-to-device copy (torch copy_, "

@@ -770,6 +770,15 @@ struct SolveOut {
 #ifndef MR_SOFT_RESTO
 #define MR_SOFT_RESTO 1
 #endif
+// IPOPT's least-square multipliers of the restoration problem at its start (RestoIterateInitializer with
+// constr_mult_init_max 1000; Solver::ls_resto, mr_wave.h ls_resto): implemented, OFF by default -- on the
+// product's restoration NLP (a two-sided row's two distances relaxed separately) the estimate
+// is not IPOPT's, and with it on the host build's statuses on the C3 sample's 23 restoration instances agree
+// with IPOPT's on 17 (wave) / 16 (scalar) against 19 / 18 off (profiles/r06_resto_rules.json); 0: the rows'
+// multipliers start at 0
+#ifndef MR_RESTO_LS_MULT
+#define MR_RESTO_LS_MULT 0
+#endif
 constexpr double IP_SOFT_RESTO_FACTOR = 0.9999;
 constexpr int IP_MAX_SOFT_RESTO = 10;
 constexpr double IP_TINY_STEP_TOL = 10.0 * 2.220446049250313e-16;
@@ -2138,6 +2147,142 @@ struct Solver {
     delta_last = T(0);
     theta_max = T(1e4) * mr_max(T(1), th_r);
     theta_min = T(1e-4) * mr_max(T(1), th_r);
+    if (MR_RESTO_LS_MULT) ls_resto();
+  }
+
+  // IPOPT's least-square multipliers of the restoration NLP at its starting point (RestoIterateInitializer ->
+  // least_square_mults, constr_mult_init_max 1000; oracle/ipopt.py _Alg.ls_mults on the restoration problem):
+  // the multipliers y minimising || grad f_R - z + J^T y ||^2 over every primal variable of the restoration
+  // NLP -- the reference's variables, the slacks and the relaxations p, n.  As in ls_init, the dual QP
+  //   min 1/2 |u|^2 + q^T u  s.t. J u = 0   (q = grad f_R - z: 0 on the variables (the proximity term's
+  //   gradient vanishes at z_R), -v on a slack, rho - v_p / rho - v_n on p / n)
+  // on the stage structure: a slot row a.sx - ss - sp + sn = 0 with (ss, sp, sn) condensed leaves
+  // (a.sx - cg)^2 / 6, cg = v + v_p - v_n, i.e. H += a a^T / 3, g -= a cg / 3, and the row multiplier
+  // y = (cg - a.sx) / 3 (the restoration rows' sign: y = v at stationarity); a relaxed vehicle row's (p, n)
+  // condensed into the disturbance w = n - p leave (w + v_p - v_n)^2 / 4: sw = 1/2, gw = (v_p - v_n) / 2.
+  // Solved by the restoration Riccati recursion and its forward sweep; the costates are the dynamics rows'
+  // multipliers.  All of them zero if one exceeds 1000 in magnitude (the rows', the vehicle rows' and the
+  // initial-state rows').
+  MR_HD void ls_resto() {
+    T z[NZS];
+    for (int k = 0; k <= N; ++k) {
+      load_z(k, cur, z);
+      T H[NH], g[NZ], J[48];
+      for (int i = 0; i < NH; ++i) H[i] = T(0);
+      for (int i = 0; i < NZ; ++i) g[i] = T(0);
+      for (int i = 0; i < 48; ++i) J[i] = T(0);
+      if (k < N) {
+        T Hd[36], fx[6], nz[NX];
+        for (int i = 0; i < NX; ++i) nz[i] = T(0);
+        Dyn<T, MODEL>::fjh(P, z, z + NX, nz, fx, J, Hd);
+        for (int i = 0; i < 6; ++i) {
+          W(k, WF::CSW + i) = T(0.5);
+          W(k, WF::CGW0 + i) = T(0.5) * (W(k, WF::CVP + i) - W(k, WF::CVN + i));
+          W(k, WF::CGW1 + i) = T(0);
+        }
+      }
+      for (int i = 0; i < NZ; ++i)
+        if (delta_var(i)) H[hidx(i, i)] = T(1);
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      T d[NI];
+      int act[NI];
+      Row<T> rows[NROW];
+      row_values(k, z, e, d, act, rows);
+      for (int r = 0; r <= NROW; ++r) {
+        const int j0 = r < NROW ? 2 * r : JL;
+        if (!act[j0]) continue;
+        int idx[3];
+        T a[3];
+        const int na = row_grad(r, rows, e, idx, a);
+        for (int sd = 0; sd < 2; ++sd) {  // slot j0 (a) and j0 + 1 (-a): each its own relaxed row
+          const int j = j0 + sd;
+          const T sg = sd ? T(-1) : T(1);
+          const T cg = W(k, WF::LAM + j) + W(k, WF::RVP + j) - W(k, WF::RVN + j);
+          for (int q = 0; q < na; ++q) {
+            g[idx[q]] -= sg * a[q] * cg / T(3);
+            for (int q2 = q; q2 < na; ++q2) H[hidx(idx[q], idx[q2])] += a[q] * a[q2] / T(3);
+          }
+        }
+      }
+      for (int i = 0; i < NH; ++i) { W(k, WF::H + i) = H[i]; W(k, WF::HD + i) = T(0); }
+      for (int i = 0; i < NZ; ++i) { W(k, WF::G0 + i) = g[i]; W(k, WF::G1 + i) = T(0); W(k, WF::GD + i) = T(0); }
+      for (int i = 0; i < NX; ++i) W(k, WF::C + i) = T(0);
+      for (int i = 0; i < 48; ++i) W(k, WF::J + i) = J[i];
+    }
+    if (!riccati(T(0))) return;  // (not positive definite on the null space: the multipliers stay 0)
+    T dx[NX];
+    for (int i = 0; i < NX; ++i) dx[i] = T(0);
+    bool ok = true;
+    const T big = T(IP_MULT_INIT_MAX);
+    double nuv[64][NX];
+    T yv[64][NI];
+    for (int k = 0; k <= N; ++k) {
+      T dz[NZS];
+      for (int i = 0; i < NZS; ++i) dz[i] = T(0);
+      for (int i = 0; i < NX; ++i) dz[i] = dx[i];
+      if (k < N)
+        for (int a = 0; a < NU; ++a) {
+          T v = W(k, WF::K0 + a);
+          for (int j = 0; j < NX; ++j) v += W(k, WF::K + a * NX + j) * dx[j];
+          dz[NX + a] = v;
+        }
+      if (k == 0)  // the initial-state rows' multipliers (dx_0 = 0): checked, not kept (x_0 is not relaxed)
+        for (int i = 0; i <= 6; ++i) ok = ok && mr_abs(W(0, WF::PV0 + i)) <= big;
+      load_z(k, cur, z);
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      T d[NI];
+      int act[NI];
+      Row<T> rows[NROW];
+      row_values(k, z, e, d, act, rows);
+      for (int j = 0; j < NI; ++j) yv[k][j] = T(0);
+      for (int r = 0; r <= NROW; ++r) {
+        const int j0 = r < NROW ? 2 * r : JL;
+        if (!act[j0]) continue;
+        int idx[3];
+        T a[3];
+        const int na = row_grad(r, rows, e, idx, a);
+        T adz = T(0);
+        for (int q = 0; q < na; ++q) adz += a[q] * dz[idx[q]];
+        for (int sd = 0; sd < 2; ++sd) {
+          const int j = j0 + sd;
+          const T cg = W(k, WF::LAM + j) + W(k, WF::RVP + j) - W(k, WF::RVN + j);
+          const T y = (cg - (sd ? -adz : adz)) / T(3);
+          yv[k][j] = y;
+          ok = ok && mr_abs(y) <= big;
+        }
+      }
+      if (k < N) {
+        T J[48], t[NX], tb[NX];
+        for (int i = 0; i < 48; ++i) J[i] = W(k, WF::J + i);
+        apply_A(J, k, dx, t);
+        apply_B(J, k, dz + NX, tb);
+        for (int i = 0; i < NX; ++i) dx[i] = t[i] + tb[i];
+        T Pn[NP], sw[6], rhs[6], w[6];
+        for (int i = 0; i < NP; ++i) Pn[i] = W(k + 1, WF::P + i);
+        for (int i = 0; i < 6; ++i) {
+          T v = W(k + 1, WF::PV0 + i);
+          for (int l = 0; l < NX; ++l) v += Pn[pidx(i, l)] * dx[l];
+          rhs[i] = v + W(k, WF::CGW0 + i);
+          sw[i] = W(k, WF::CSW + i);
+        }
+        noise_step(Pn, sw, rhs, w);
+        for (int i = 0; i < 6; ++i) dx[i] += w[i];
+        for (int i = 0; i < NX; ++i) {  // the multipliers of x_{k+1} = F(x_k, u_k) (+ n - p)
+          T v = W(k + 1, WF::PV0 + i);
+          for (int l = 0; l < NX; ++l) v += Pn[pidx(i, l)] * dx[l];
+          nuv[k + 1][i] = (double)v;
+          if (i < 6) ok = ok && mr_abs(v) <= big;
+        }
+      }
+    }
+    if (!ok) return;
+    for (int k = 0; k <= N; ++k) {
+      for (int j = 0; j < NI; ++j) W(k, WF::RY + j) = yv[k][j];
+      if (k >= 1)
+        for (int i = 0; i < NX; ++i) nub[k][i] = nuv[k][i];
+    }
   }
   MR_HD bool resto_done() const {  // the accepted restoration step's point, seen by the original problem
     if (!(tho_acc <= T(RESTO_KAPPA) * th_entry)) return false;

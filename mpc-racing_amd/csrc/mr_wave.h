@@ -2462,6 +2462,133 @@ struct WaveSolver {
     theta_max = T(1e4) * mr_max(T(1), th_r);
     theta_min = T(1e-4) * mr_max(T(1), th_r);
     wsync(w);
+    if (MR_RESTO_LS_MULT) ls_resto();
+  }
+
+  // IPOPT's least-square multipliers of the restoration NLP at its start (mr_solver.h Solver::ls_resto, the
+  // derivation there): the stage QP H = I on the reference's variables + a a^T / 3 per relaxed row slot,
+  // g = -a cg / 3 (cg = v + v_p - v_n), the vehicle rows' disturbance with sw = 1/2, gw = (v_p - v_n) / 2,
+  // solved by the restoration Riccati and forward sweeps; y = (cg - a.sx) / 3, the costates the dynamics rows'
+  // multipliers; all zero if one exceeds 1000.  Run once per restoration phase, by few instances.
+  MR_SWEEP void ls_record_resto() {
+    MR_UNIFORM_P();
+    MR_ASSUME_LDS_STATE();
+    if (own()) {
+      const int k = ln;
+      T z[NZS];
+      load_z(cur, z);
+      MR_GLOBAL T* Rk = R(k);
+      T H[NH], g[NZ];
+      for (int i = 0; i < NH; ++i) H[i] = T(0);
+      for (int i = 0; i < NZ; ++i) g[i] = T(0);
+      if (k < N) {
+        T Hd[36], fx[6], J[48], nz[NX];
+        for (int i = 0; i < NX; ++i) nz[i] = T(0);
+        Dyn<T, MODEL>::fjh(P, z, z + NX, nz, fx, J, Hd);
+        for (int i = 0; i < 48; ++i) Rk[RCF::J + i] = J[i];
+        for (int i = 0; i < 6; ++i) {
+          Cf(CSF::CSW + i) = T(0.5);
+          Cf(CSF::CGW0 + i) = T(0.5) * (Cf(CSF::CVP + i) - Cf(CSF::CVN + i));
+          Cf(CSF::CGW1 + i) = T(0);
+        }
+      }
+      for (int i = 0; i < NZ; ++i)
+        if (delta_var(i)) H[hidx(i, i)] = T(1);
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      T d[NI];
+      int act[NI];
+      row_values(k, z, e, d, act);
+      auto cg = [&](int j) { return S(SSF::LAM + j) + Cf(CSF::RVP + j) - Cf(CSF::RVN + j); };
+#pragma unroll
+      for (int r = 0; r < NROW; ++r) {
+        if (!act[2 * r]) continue;
+        const T gs = (cg(2 * r) - cg(2 * r + 1)) / T(3);  // slot 2r on +a, slot 2r + 1 on -a
+#pragma unroll
+        for (int a = 0; a < RN(r); ++a) {
+          g[RI(r, a)] -= T(RS(a)) * gs;
+#pragma unroll
+          for (int bb = a; bb < RN(r); ++bb) H[hidx(RI(r, a), RI(r, bb))] += T(2) / T(3) * T(RS(a)) * T(RS(bb));
+        }
+      }
+      if (lane_active(P, k)) {
+        const int id3[3] = {0, 1, 6};
+        const T gs = (cg(JL) - cg(JL + 1)) / T(3);
+        for (int a = 0; a < 3; ++a) {
+          g[id3[a]] -= e.gC[a] * gs;
+          for (int bb = a; bb < 3; ++bb) H[hidx(id3[a], id3[bb])] += T(2) / T(3) * e.gC[a] * e.gC[bb];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < NHC; ++q) Rk[RCF::H + q] = H[HCT.p[q]];
+      for (int i = 0; i < NZ; ++i) { Rk[RCF::G0 + i] = g[i]; Rk[RCF::G1 + i] = T(0); Rk[RCF::GD + i] = T(0); }
+      for (int i = 0; i < NX; ++i) Rk[RCF::C + i] = T(0);
+    }
+    wsync(w);
+  }
+  MR_SWEEP void ls_finish_resto() {
+    MR_UNIFORM_P();
+    MR_ASSUME_LDS_STATE();
+    const T big = T(IP_MULT_INIT_MAX);
+    int ok_l = 1;
+    T yv[NI];
+    for (int j = 0; j < NI; ++j) yv[j] = T(0);
+    if (own()) {
+      const int k = ln;
+      T z[NZS], dz[NZS];
+      load_z(cur, z);
+      for (int i = 0; i < NZS; ++i) dz[i] = S(SSF::DZ + i);
+      Err<T> e;
+      errors(I, z[0], z[1], z[6], e, false);
+      T d[NI];
+      int act[NI];
+      row_values(k, z, e, d, act);
+      auto cg = [&](int j) { return S(SSF::LAM + j) + Cf(CSF::RVP + j) - Cf(CSF::RVN + j); };
+#pragma unroll
+      for (int r = 0; r < NROW; ++r) {
+        if (!act[2 * r]) continue;
+        const T adz = row_c(r, dz);
+        yv[2 * r] = (cg(2 * r) - adz) / T(3);
+        yv[2 * r + 1] = (cg(2 * r + 1) + adz) / T(3);
+      }
+      if (lane_active(P, k)) {
+        const T adz = e.gC[0] * dz[0] + e.gC[1] * dz[1] + e.gC[2] * dz[6];
+        yv[JL] = (cg(JL) - adz) / T(3);
+        yv[JL + 1] = (cg(JL + 1) + adz) / T(3);
+      }
+      for (int j = 0; j < NI; ++j) ok_l &= mr_abs(yv[j]) <= big ? 1 : 0;
+      if (k >= 1)
+        for (int i = 0; i < 6; ++i) ok_l &= mr_abs(S(SSF::DNU + i)) <= big ? 1 : 0;
+      else  // the initial-state rows' multipliers (dx_0 = 0: stage 0's costate), checked, not kept
+        for (int i = 0; i <= 6; ++i) ok_l &= mr_abs(R(0)[RCF::PV0 + i]) <= big ? 1 : 0;
+    }
+    const bool ok = wall(w, ok_l != 0);
+    if (own()) {
+      const int k = ln;
+      for (int i = 0; i < NX; ++i) {
+        if (ok && k >= 1) NUd(i) = (double)S(SSF::DNU + i);
+        S(SSF::DNU + i) = T(0);
+      }
+      for (int i = 0; i < NZS; ++i) S(SSF::DZ + i) = T(0);
+      for (int j = 0; j < NI; ++j) {
+        if (ok) Cf(CSF::RY + j) = yv[j];
+        Cf(CSF::RDY + j) = T(0);
+        Cf(CSF::RDP + j) = T(0); Cf(CSF::RDN + j) = T(0); Cf(CSF::RDVP + j) = T(0); Cf(CSF::RDVN + j) = T(0);
+        S(SSF::DS + j) = T(0);
+        S(SSF::DLAM + j) = T(0);
+      }
+      for (int i = 0; i < 6; ++i) {
+        Cf(CSF::CDP + i) = T(0); Cf(CSF::CDN + i) = T(0); Cf(CSF::CDVP + i) = T(0); Cf(CSF::CDVN + i) = T(0);
+      }
+    }
+    wsync(w);
+  }
+  MR_HD void ls_resto() {
+    ls_record_resto();
+    if (!riccati<true>(T(0), mu)) return;  // (not positive definite on the null space: the multipliers stay 0)
+    T ap, ad, gphi;
+    forward_resto(ap, ad, gphi);
+    ls_finish_resto();
   }
   MR_HD bool resto_done() {  // the accepted restoration step's point, seen by the original problem
     auto* C = cw();

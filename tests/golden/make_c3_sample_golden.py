@@ -13,7 +13,7 @@ iterations, restoration iterations, objective, U / X / S.  tests/test_gpu_golden
 the IPOPT outcomes (status class on the sample, solutions where both solve); the PRODUCT columns are the
 audit of the remaining deviations (do they change outcomes?).
 
-Usage: python tests/golden/make_c3_sample_golden.py [--procs=8]
+Usage: python tests/golden/make_c3_sample_golden.py [--procs=8] [--rules=IPOPT,PRODUCT]
 """
 import json
 import os
@@ -59,12 +59,16 @@ def _solve(args):
 
 def main():
     procs = int(next((a.split("=")[1] for a in sys.argv[1:] if a.startswith("--procs=")), 8))
+    # --rules=PRODUCT: re-solve one column only and keep the fixture's other columns (a change of PRODUCT does not
+    # move the IPOPT column)
+    rules = tuple(next((a.split("=")[1] for a in sys.argv[1:] if a.startswith("--rules=")), ",".join(RULES)).split(","))
     idx = sample_indices()
-    jobs = [(j, rn) for rn in RULES for j in idx]
+    jobs = [(j, rn) for rn in rules for j in idx]
     with Pool(procs) as pool:
         res = pool.map(_solve, jobs, chunksize=1)
-    out = {"idx": np.array(idx, dtype=np.int64)}
-    for rn in RULES:
+    out = dict(np.load(OUT)) if os.path.exists(OUT) else {}
+    out["idx"] = np.array(idx, dtype=np.int64)
+    for rn in rules:
         rs = [r for (j, n), r in zip(jobs, res) if n == rn]
         for k in ("X", "U", "S"):
             out[f"{rn}_{k}"] = np.stack([r[k] for r in rs], axis=-1)
