@@ -3,6 +3,7 @@ instances left at max_iter / status 3 / status 4, and the solve's wall time (the
 the reference's tol 1e-4 / acceptable_tol 1e-2 / acceptable_iter 15 unless overridden).
 
 Usage: python mpc-racing_amd/tools/status_census.py C3 C4 C5 [--tol 1e-8] [--out gpurun_out/census.json]
+       [--npz gpurun_out/census]   (every instance's status and iteration count)
 """
 import argparse
 import json
@@ -21,6 +22,7 @@ def main():
     ap.add_argument("configs", nargs="+")
     ap.add_argument("--tol", type=float, default=None)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--npz", default=None, help="also save every instance's status / iterations: <npz>_<config>.npz")
     a = ap.parse_args()
     import torch
     from mpcracing import workload as wl
@@ -49,6 +51,8 @@ def main():
                "status4_instances": np.where(st == 4)[0].tolist()[:64]}
         print(json.dumps(rec), flush=True)
         recs.append(rec)
+        if a.npz:
+            np.savez(f"{a.npz}_{name}.npz", status=st, iters=it)
     if a.out:
         with open(a.out, "w") as f:
             for r in recs:
