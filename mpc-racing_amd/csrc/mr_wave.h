@@ -65,8 +65,8 @@
 #define MR_PHASE_CYCLES 0  // 1: per-sweep shader-cycle counters of the trace instance (tools/phase_probe.py)
 #endif
 // trace rows reserved at the end of a trace buffer: the final status record's slack row and the cycle rows
-// (MR_PHASE_CYCLES: rows trace_cap - 1 .. trace_cap - 3), never overwritten by per-iteration rows
-#define MR_TRACE_RESERVED (MR_PHASE_CYCLES ? 3 : 2)
+// (MR_PHASE_CYCLES: rows trace_cap - 1 .. trace_cap - 4), never overwritten by per-iteration rows
+#define MR_TRACE_RESERVED (MR_PHASE_CYCLES ? 4 : 2)
 
 namespace mr {
 
@@ -303,7 +303,7 @@ struct WaveSolver {
   double* trace = nullptr;
   int trace_cap = 0;
 #if MR_PHASE_CYCLES
-  unsigned long long tsub[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // diagnostics: sub-phase cycles of the trace instance
+  unsigned long long tsub[24] = {};  // diagnostics: sub-phase cycles of the trace instance
 #endif
 
   MR_HD WaveSolver(const MR_CONST ProbParams<T>& P_, const Inst<T>& I_, Wv w_, MR_GLOBAL T* ws, MR_LDS T* lds_,
@@ -1667,7 +1667,7 @@ struct WaveSolver {
   //   LS_ACC    one trial, accumulate its constraint values into the SOC right-hand sides
   //             (SC = acc SC + c(trial), SR = acc SR + (d - s)(trial)), nothing stored;
   //   LS_CAP    the first trial's constraint values are also written to the cold fields CTR / CTC, so a
-  //             second-order correction of that trial point accumulates them (soc_accumulate) instead of
+  //             second-order correction of that trial point accumulates them (soc_backward) instead of
   //             evaluating the point again;
   //   otherwise backtracking; a rejected first trial (a0 = the fraction-to-boundary step, theta not
   //   decreased) returns with LS_NEED_SOC so the caller runs the second-order corrections.
@@ -1978,44 +1978,15 @@ struct WaveSolver {
   // ---------------- second-order corrections (IPOPT's TrySecondOrderCorrection, linear) ----------------
   // mr_solver.h Solver::try_soc / soc_backward: the Newton system re-solved on the stored factorisation
   // with the constraint right-hand sides c_soc (dynamics rows, CSF::SC) and r_soc (the rows' d - s,
-  // CSF::SR), c_soc = alpha c_soc + c(trial) per correction.  Run by few instances for few iterations, so
-  // the sequential parts are wave-uniform (every lane computes the same, the record read with uniform
-  // addresses) -- written for clarity, like forward_resto.
-  // c_soc, r_soc at the current point (lane = stage)
-  MR_SWEEP void soc_prepare() {
-    MR_UNIFORM_P();
-    MR_ASSUME_LDS_STATE();
-    if (own()) {
-      const int k = ln;
-      for (int i = 0; i < NX; ++i) Cf(CSF::SC + i) = k < N ? R(k)[RCF::C + i] : T(0);
-      T z[NZS];
-      load_z(cur, z);
-      Err<T> e;
-      errors(I, z[0], z[1], z[6], e, false);
-      T d[NI];
-      int act[NI];
-      row_values(k, z, e, d, act);
-      for (int j = 0; j < NI; ++j)
-        Cf(CSF::SR + j) = (act[j] && yslot(j)) ? T(slot_sign(j)) * (d[j] - S(sf(cur) + j)) : T(0);
-    }
-    wsync(w);
-  }
-  // SC = acc SC + c(trial), SR = acc SR + (d - s)(trial) from the values the trial's evaluation captured
-  // (LS_CAP; 0 where LS_ACC's evaluation accumulates nothing, so the fields it leaves alone stay 0)
-  MR_SWEEP void soc_accumulate(T acc) {
-    MR_ASSUME_LDS_STATE();
-    if (own()) {
-      for (int j = 0; j < NI; ++j) Cf(CSF::SR + j) = acc * Cf(CSF::SR + j) + Cf(CSF::CTR + j);
-      for (int i = 0; i < NX; ++i) Cf(CSF::SC + i) = acc * Cf(CSF::SC + i) + Cf(CSF::CTC + i);
-    }
-    wsync(w);
-  }
+  // CSF::SR), c_soc = alpha c_soc + c(trial) per correction (accumulated in soc_backward's stage-parallel pass).
+  // Up to max_soc = 4 per iteration; the batch's long solves run 2-3 per iteration, so the two recursions
+  // (socb_chain backward, fwd_recursion<true> forward) are lane recursions on the stage records.
   // The SOC costate recursion given v_k, u_k (cold fields SPV, SK0: everything that does not depend on
   // pv_{k+1}): lane i < NX forms pv_k[i] = v_k[i] + (A_k^T pv_{k+1})[i] + sum_a K_k[a][i] (B_k^T pv_{k+1})[a]
   // from pv_{k+1} broadcast by v_readlane; B_k^T pv_{k+1} (the same in every lane) plus u_k is r_k, the
   // feed-forward's right-hand side.  Results to LDS only (pv_k to LDX row k, r_k to [LX_OFF + 3 k]): no
   // global stores in the loop, so the in-order vmcnt waits for the prefetched operands stay exact.  Per
-  // stage: one broadcast of pv (11 v_readlane), ~25 FMAs, 23 buffer loads issued three stages ahead.
+  // stage: one broadcast of pv (11 v_readlane), ~25 FMAs, 23 buffer loads issued two stages ahead.
   MR_HD void socb_chain() {
     const int N = wu(this->w, this->N), ln = this->ln;
     const Wv w = this->w;
@@ -2121,7 +2092,9 @@ struct WaveSolver {
   // lanes 0..10 (lane i: component i of pc / pv, the others' by v_readlane), every lane gathering its
   // row of P_{k+1}, its column of A_k and K_k from the stage's record (a few cache lines per stage) and
   // the shared terms (B's J columns, Q_uu's factor, c_k, g_u) as uniform loads, one stage ahead.
-  MR_SWEEP void soc_backward() {
+  // first: the episode's first correction (its right-hand sides start from the current point); acc: the
+  // previous trial's step size (IPOPT: c_soc = alpha c_soc + c(trial), r_soc likewise)
+  MR_SWEEP void soc_backward(bool first, T acc) {
     MR_UNIFORM_P();
     MR_ASSUME_LDS_STATE();
 #if MR_PHASE_CYCLES
@@ -2144,15 +2117,42 @@ struct WaveSolver {
       T d[NI];
       int act[NI];
       row_values(k, z, e, d, act);
+      // the right-hand sides c_soc (dynamics rows, SC) and r_soc (the rows' d - s, SR): on the episode's first
+      // correction the current point's values, then accumulated with the trial point's values its evaluation
+      // captured (LS_CAP; 0 where nothing is accumulated) -- in this stage-parallel pass, which evaluates the
+      // current point's rows anyway (a separate prepare / accumulate sweep cost two round trips per correction).
+      // Every operand loaded unconditionally first, then selected: no load waited for inside a per-slot branch
+      T srv[NI], ctr[NI], slk[NI], scv[NX], ctc[NX], cdef[NX];
+      for (int j = 0; j < NI; ++j) {
+        srv[j] = Cf(CSF::SR + j);
+        ctr[j] = Cf(CSF::CTR + j);
+        slk[j] = S(sf(cur) + j);
+      }
+      for (int i = 0; i < NX; ++i) {
+        scv[i] = Cf(CSF::SC + i);
+        ctc[i] = Cf(CSF::CTC + i);
+        cdef[i] = Rk[RCF::C + i];
+      }
+      T sr[NI];
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const T p0 = (act[j] && yslot(j)) ? T(slot_sign(j)) * (d[j] - slk[j]) : T(0);
+        sr[j] = acc * (first ? p0 : srv[j]) + ctr[j];
+      }
+      T scn[NX];
+#pragma unroll
+      for (int i = 0; i < NX; ++i) scn[i] = acc * (first ? (k < N ? cdef[i] : T(0)) : scv[i]) + ctc[i];
+      for (int j = 0; j < NI; ++j) Cf(CSF::SR + j) = sr[j];
+      for (int i = 0; i < NX; ++i) Cf(CSF::SC + i) = scn[i];
 #pragma unroll
       for (int r = 0; r <= NROW; ++r) {
         const int j0 = r < NROW ? 2 * r : JL, j1 = j0 + 1;
         if (!act[j0]) continue;
-        const T t0 = S(sf(cur) + j0), t1 = S(sf(cur) + j1);
+        const T t0 = slk[j0], t1 = slk[j1];
         const T s0 = S(SSF::LAM + j0) / t0, s1 = S(SSF::LAM + j1) / t1;
         T dg;
-        if (r < 2) dg = (s0 + dl) * (Cf(CSF::SR + j0) - (d[j0] - t0)) + (s1 + dl) * (Cf(CSF::SR + j1) + (d[j1] - t1));
-        else dg = (s0 + s1 + dl) * (Cf(CSF::SR + j0) - (d[j0] - t0));
+        if (r < 2) dg = (s0 + dl) * (sr[j0] - (d[j0] - t0)) + (s1 + dl) * (sr[j1] + (d[j1] - t1));
+        else dg = (s0 + s1 + dl) * (sr[j0] - (d[j0] - t0));
         if (r < NROW) {
 #pragma unroll
           for (int a = 0; a < RN(r); ++a) g[RI(r, a)] += T(RS(a)) * dg;
@@ -3114,7 +3114,14 @@ struct WaveSolver {
             accepted = (flags & LSR_ACC) != 0;
           }
         } else {
+#if MR_PHASE_CYCLES
+          unsigned long long tq = trace ? MR_CLOCK() : 0ull;
+#define MR_TQ(q) do { if (trace) { const unsigned long long tn = MR_CLOCK(); tsub[q] += tn - tq; tq = tn; } } while (0)
+#else
+#define MR_TQ(q) ((void)0)
+#endif
           line_search<false, false>(th, ph, gphi, th_pow, ap, ap, a_min, 0, LS_CAP, T(0), T(-1));
+          MR_TQ(16);
           flags = res_flags;
           rejf |= (flags & LSR_REJF) != 0;
           accepted = (flags & LSR_ACC) != 0;
@@ -3123,19 +3130,21 @@ struct WaveSolver {
             // kappa_soc (0.99); then, if none is accepted, the backtracking resumes at alpha / 2
             const T a_trial = res_alpha, a_test0 = res_atest;
             T th_trial = res_th, a_soc = a_trial, th_old = T(0);
-            soc_prepare();
+#if MR_PHASE_CYCLES
+            if (trace) { tsub[22] += 1; tq = MR_CLOCK(); }
+#endif
             for (int count = 0; count < IP_MAX_SOC; ++count) {
               if (count > 0 && !(th_trial <= T(IP_KAPPA_SOC) * th_old)) break;
               th_old = th_trial;
               // the trial point's constraint values: captured by its own evaluation (the first trial of the
-              // line search, or the previous correction's trial)
-              soc_accumulate(a_soc);
+              // line search, or the previous correction's trial), accumulated by soc_backward
+              MR_TQ(17);
               MR_STAT(st_soc_try++);
               MR_CNT(5);
 #if MR_PHASE_CYCLES
               const unsigned long long ts0 = trace ? MR_CLOCK() : 0ull;
 #endif
-              soc_backward();
+              soc_backward(count == 0, a_soc);
 #if MR_PHASE_CYCLES
               const unsigned long long ts1 = trace ? MR_CLOCK() : 0ull;
 #endif
@@ -3144,8 +3153,12 @@ struct WaveSolver {
 #if MR_PHASE_CYCLES
               if (trace) { tsub[6] += ts1 - ts0; tsub[7] += MR_CLOCK() - ts1; }
 #endif
+#if MR_PHASE_CYCLES
+              if (trace) tq = MR_CLOCK();
+#endif
               line_search<false, true>(th, ph, gphi, th_pow, aps, aps, aps, 0, LS_WD | LS_CAP,
                                        a_test0, T(-1));
+              MR_TQ(18);
               rejf |= (res_flags & LSR_REJF) != 0;
               a_soc = aps;
               if (!(res_flags & LSR_FIN)) break;
@@ -3153,12 +3166,17 @@ struct WaveSolver {
                 soc_taken = accepted = true;
                 flags = res_flags;
                 ad = soc_commit();
+                MR_TQ(19);
                 break;
               }
               th_trial = res_th;
             }
             if (!soc_taken) {
+#if MR_PHASE_CYCLES
+              if (trace) { tsub[23] += 1; tq = MR_CLOCK(); }
+#endif
               line_search<false, false>(th, ph, gphi, th_pow, T(0.5) * a_trial, ap, a_min, 1, LS_NOSOC, T(0), T(-1));
+              MR_TQ(20);
               flags = res_flags;
               rejf |= (flags & LSR_REJF) != 0;
               accepted = (flags & LSR_ACC) != 0;
@@ -3167,7 +3185,13 @@ struct WaveSolver {
         }
         if (MR_SOFT_RESTO && !accepted && !take_anyway) {
           // IPOPT's soft restoration phase before the restoration phase proper (TrySoftRestoStep)
+#if MR_PHASE_CYCLES
+          const unsigned long long tsr = trace ? MR_CLOCK() : 0ull;
+#endif
           const int sr = soft_resto(th, ph, gphi, th_pow, ap, ad);
+#if MR_PHASE_CYCLES
+          if (trace) tsub[21] += MR_CLOCK() - tsr;
+#endif
           if (sr) {
             accepted = soft_step = true;
             soft_orig = sr == 1;
@@ -3255,6 +3279,7 @@ struct WaveSolver {
 #undef MR_T0
 #undef MR_T1
 #undef MR_CNT
+#undef MR_TQ
 #if MR_PHASE_CYCLES
     if (trace && ln == 0 && trace_cap >= 2) {  // last row: cycles eval, riccati, forward, trial, #trials, #soc, #factorisations, total
       double* tr = trace + 8 * (trace_cap - 1);
@@ -3265,6 +3290,12 @@ struct WaveSolver {
       if (trace_cap >= 3) {  // trial sub-phases: stage values, reductions, acceptance tests; line-search setup
         double* tr3 = trace + 8 * (trace_cap - 3);
         for (int q = 0; q < 8; ++q) tr3[q] = (double)tsub[8 + q];
+      }
+      if (trace_cap >= 4) {  // line-search phase split: first line search, SOC accumulation (0 since it moved
+        // into soc_backward), SOC trial line searches, SOC commit, resumed backtracking, soft restoration; #SOC
+        // episodes, #resumed line searches
+        double* tr4 = trace + 8 * (trace_cap - 4);
+        for (int q = 0; q < 8; ++q) tr4[q] = (double)tsub[16 + q];
       }
     }
 #endif

@@ -6,6 +6,7 @@ bounds of mpcracing.hip): variants/lib_<name>.so, run by tools/gpu_flags_ab.sh o
   slp      SLP vectorisation on (no -fno-slp-vectorize)
   w1       fp32 solve kernel at 1 wave per SIMD (MR_WAVES_PER_SIMD_F32=1, 512 VGPRs)
   cyc      per-sweep shader-cycle counters of the trace instance (tools/phase_probe.py)
+  nofma    no floating-point contraction (-ffp-contract=off: the host build's arithmetic, no FMA)
 """
 import os
 import sys
@@ -22,6 +23,7 @@ VARIANTS = {
     "slp": [f for f in DEFAULT_FLAGS if f != "-fno-slp-vectorize"],
     "w1": DEFAULT_FLAGS + ["-DMR_WAVES_PER_SIMD_F32=1"],
     "cyc": DEFAULT_FLAGS + ["-DMR_PHASE_CYCLES=1"],
+    "nofma": ["-ffp-contract=off"] + [f for f in DEFAULT_FLAGS if not f.startswith("-ffp-contract")],
 }
 
 

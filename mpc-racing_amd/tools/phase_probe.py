@@ -21,6 +21,9 @@ from mpcracing import workload as wl  # noqa: E402
 from mpcracing.batch import solver_for_config  # noqa: E402
 
 NAMES = ["eval", "riccati", "forward", "trial", "n_trials", "n_soc_tries", "n_fact", "total"]
+# the fourth diagnostics row (mr_wave.h MR_PHASE_CYCLES): the line-search phase by call
+LS_SPLIT = ["ls_first", "soc_prep_acc", "ls_soc", "soc_commit", "ls_resume", "soft_resto", "n_soc_episodes",
+            "n_ls_resume"]
 
 
 def _solver(name, B):
@@ -58,6 +61,7 @@ def one(name, b, i, cap=520):
                         "soc_backward", "soc_forward"], tr[-2][:8].tolist())))
     row.update(dict(zip(["trial_stage", "trial_reduce", "trial_accept", "ls_setup", "socb_grad", "socb_pre", "socb_chain",
                           "socb_post"], tr[-3][:8].tolist())))
+    row.update(dict(zip(LS_SPLIT, tr[-4][:8].tolist())))
     row.update(instance=i, iters=it, status=int(out["status"][0]), wall_ms=1e3 * min(lat),
                cycles_per_iter=row["total"] / max(it, 1))
     return row
@@ -88,6 +92,7 @@ def main():
                                  "n_fact_failed", "soc_backward", "soc_forward"], tr[-2][:8].tolist())))
             row.update(dict(zip(["trial_stage", "trial_reduce", "trial_accept", "ls_setup", "socb_grad", "socb_pre", "socb_chain",
                           "socb_post"], tr[-3][:8].tolist())))
+            row.update(dict(zip(LS_SPLIT, tr[-4][:8].tolist())))
             row.update(instance=i, iters=it_i, status=int(o["status"][i]), in_batch=True,
                        cycles_per_iter=row["total"] / max(it_i, 1))
             res[name].append(row)
