@@ -1664,8 +1664,6 @@ struct WaveSolver {
   //   LS_WD     one trial, judged at the given test step size (the watchdog's, or the SOC's original), and
   //             stored whatever its acceptance (the watchdog's tentative full step needs no re-evaluation);
   //   LS_FORCE  one trial, stored whatever its acceptance;
-  //   LS_ACC    one trial, accumulate its constraint values into the SOC right-hand sides
-  //             (SC = acc SC + c(trial), SR = acc SR + (d - s)(trial)), nothing stored;
   //   LS_CAP    the first trial's constraint values are also written to the cold fields CTR / CTC, so a
   //             second-order correction of that trial point accumulates them (soc_backward) instead of
   //             evaluating the point again;
@@ -1673,11 +1671,10 @@ struct WaveSolver {
   //   decreased) returns with LS_NEED_SOC so the caller runs the second-order corrections.
   // SOCDIR: the trial points lie along the SOC direction (SDZ, SDS) instead of the Newton direction.
   // RESTO: the restoration phase's NLP (mr_solver.h trial() with resto set).
-  enum { LS_WD = 1, LS_FORCE = 2, LS_ACC = 4, LS_NOSOC = 8, LS_CAP = 16 };
+  enum { LS_WD = 1, LS_FORCE = 2, LS_NOSOC = 8, LS_CAP = 16 };
   enum { LSR_ACC = 1, LSR_AUG = 2, LSR_REJF = 4, LSR_NEED_SOC = 8, LSR_FIN = 16 };
   template <bool RESTO, bool SOCDIR>
-  MR_SWEEP void line_search(T th, T ph, T gphi, T th_pow, T a0, T a_max, T a_min, int nls0, int mode, T a_fix,
-                            T acc) {
+  MR_SWEEP void line_search(T th, T ph, T gphi, T th_pow, T a0, T a_max, T a_min, int nls0, int mode, T a_fix) {
     MR_UNIFORM_P();
     MR_ASSUME_LDS_STATE();
 #if MR_PHASE_CYCLES
@@ -1744,8 +1741,11 @@ struct WaveSolver {
     T zt[NZS], st[NI];
     const T kdm = T(IP_KAPPA_D) * mu;
     // one trial point: zt, st (registers), theta, phi; false if a slack is not positive or a value is
-    // not finite.  accum: add its constraint values to the SOC right-hand sides (SC, SR)
-    auto eval = [&](T alpha, bool accum, T& th_t, T& ph_t, bool cap) -> bool {
+    // not finite.  CAP (compile-time: std::true_type / false_type): also write its constraint values to the
+    // cold fields CTR / CTC for a second-order correction (LS_CAP) -- two instantiations, so the regular
+    // trials carry no per-slot store branches
+    auto eval = [&](T alpha, T& th_t, T& ph_t, auto CAPT) -> bool {
+      constexpr bool cap = decltype(CAPT)::value;
 #if MR_PHASE_CYCLES
       const unsigned long long te0 = trace ? MR_CLOCK() : 0ull;
 #endif
@@ -1778,9 +1778,8 @@ struct WaveSolver {
             if (yslot(j)) {
               const T r = d[j] - sj;
               th_l += a ? mr_abs(r) : T(0);
-              if (accum && a) Cf(CSF::SR + j) = acc * Cf(CSF::SR + j) + T(slot_sign(j)) * r;
-              if (cap) Cf(CSF::CTR + j) = a ? T(slot_sign(j)) * r : T(0);
-            } else if (cap) {
+              if constexpr (cap) Cf(CSF::CTR + j) = a ? T(slot_sign(j)) * r : T(0);
+            } else if constexpr (cap) {
               Cf(CSF::CTR + j) = T(0);
             }
           }
@@ -1788,10 +1787,7 @@ struct WaveSolver {
         for (int j = 0; j < NI; ++j) {
           if (!RESTO) break;  // (the regular trial's slots: the branch-free loop above)
           st[j] = s_c[j];
-          if (!((actm >> j) & 1u)) {
-            if (!RESTO && cap) Cf(CSF::CTR + j) = T(0);
-            continue;
-          }
+          if (!((actm >> j) & 1u)) continue;
           const T sj = s_c[j] + alpha * ds[j];
           if (!(sj > T(0))) ok_l = 0;
           st[j] = sj;
@@ -1804,12 +1800,6 @@ struct WaveSolver {
             if (yslot(j)) tho_l += mr_abs(d[j] - sj);
             lgr_l += mr_log(pt > T(0) ? pt : T(1)) + mr_log(nt > T(0) ? nt : T(1));
             f_l += rho * (pt + nt);
-          } else if (yslot(j)) {
-            th_l += mr_abs(d[j] - sj);
-            if (accum) Cf(CSF::SR + j) = acc * Cf(CSF::SR + j) + T(slot_sign(j)) * (d[j] - sj);
-            if (cap) Cf(CSF::CTR + j) = T(slot_sign(j)) * (d[j] - sj);
-          } else if (cap) {
-            Cf(CSF::CTR + j) = T(0);
           }
         }
         if constexpr (RESTO) {
@@ -1837,11 +1827,10 @@ struct WaveSolver {
           } else {
             for (int i = 0; i < NX; ++i) {
               th_l += mr_abs(xn[i] - ztn[i]);
-              if (accum) Cf(CSF::SC + i) = acc * Cf(CSF::SC + i) + (xn[i] - ztn[i]);
-              if (cap) Cf(CSF::CTC + i) = xn[i] - ztn[i];
+              if constexpr (cap) Cf(CSF::CTC + i) = xn[i] - ztn[i];
             }
           }
-        } else if (!RESTO && cap) {
+        } else if constexpr (!RESTO && cap) {
           for (int i = 0; i < NX; ++i) Cf(CSF::CTC + i) = T(0);
         }
       }
@@ -1882,18 +1871,20 @@ struct WaveSolver {
     int nls = nls0, ntr = 0;
     int flags = 0;
     bool store = false;
-    if (mode & (LS_FORCE | LS_ACC)) {
+    if (mode & LS_FORCE) {
       alpha = a_fix;
-      const bool fin = eval(alpha, (mode & LS_ACC) != 0, th_t, ph_t, false);
+      const bool fin = eval(alpha, th_t, ph_t, std::false_type{});
       ntr++;
       flags |= fin ? LSR_FIN : 0;
-      store = (mode & LS_FORCE) != 0;
-      if (store) ph_acc = ph_t;  // (the forced trial's own barrier objective: the soft restoration's test)
+      store = true;
+      ph_acc = ph_t;  // (the forced trial's own barrier objective: the soft restoration's test)
     } else {
+      const bool capm = !RESTO && (mode & LS_CAP);
       for (int n = 0; n < IP_LS_MAX; ++n) {
         if (!(alpha > a_min || n == 0)) break;
         a_test = (mode & LS_WD) ? a_fix : alpha;
-        const bool fin = eval(alpha, false, th_t, ph_t, !RESTO && (mode & LS_CAP) && n == 0);
+        const bool fin = (capm && n == 0) ? eval(alpha, th_t, ph_t, std::true_type{})
+                                          : eval(alpha, th_t, ph_t, std::false_type{});
         ntr++;
 #if MR_PHASE_CYCLES
         const unsigned long long ta0 = trace ? MR_CLOCK() : 0ull;
@@ -1982,86 +1973,69 @@ struct WaveSolver {
   // Up to max_soc = 4 per iteration; the batch's long solves run 2-3 per iteration, so the two recursions
   // (socb_chain backward, fwd_recursion<true> forward) are lane recursions on the stage records.
   // The SOC costate recursion given v_k, u_k (cold fields SPV, SK0: everything that does not depend on
-  // pv_{k+1}): lane i < NX forms pv_k[i] = v_k[i] + (A_k^T pv_{k+1})[i] + sum_a K_k[a][i] (B_k^T pv_{k+1})[a]
-  // from pv_{k+1} broadcast by v_readlane; B_k^T pv_{k+1} (the same in every lane) plus u_k is r_k, the
-  // feed-forward's right-hand side.  Results to LDS only (pv_k to LDX row k, r_k to [LX_OFF + 3 k]): no
-  // global stores in the loop, so the in-order vmcnt waits for the prefetched operands stay exact.  Per
-  // stage: one broadcast of pv (11 v_readlane), ~25 FMAs, 23 buffer loads issued two stages ahead.
+  // pv_{k+1}): pv_k = v_k + A_k^T pv_{k+1} + K_k^T b_k with b_k = B_k^T pv_{k+1}, and r_k = b_k + u_k (the
+  // feed-forward's right-hand side).  Two lane groups share one 11-term dot product with pv_{k+1} (broadcast
+  // from lanes 0..10 by v_readlane), each lane gathering its coefficient column of the stage map E^ from the
+  // record (ehat_slot: its data word or the record's constant slots): group 0 (lanes 0..10) column i of A_k
+  // -> (A_k^T pv)[i], group 1 (lanes 16..18) column a of B_k -> b_k[a]; then group 0 adds K_k^T b_k with b_k
+  // read from group 1 (the forward recursion's structure, transposed).  B_k^T pv is thus three lanes' dot
+  // products instead of twelve FMAs in every lane.  Per stage: 14 v_readlane, ~16 FMAs, 15 single-line
+  // gathers issued two stages ahead; results to LDS only (pv_k to LDX row k, r_k to [LX_OFF + 3 k]), so the
+  // in-order vmcnt waits for the prefetched operands stay exact.
   MR_HD void socb_chain() {
     const int N = wu(this->w, this->N), ln = this->ln;
     const Wv w = this->w;
     const WBuf<T> wb(rc - (int64_t)SSF::NF * WL, (unsigned)WS_NU_OFF);
     auto R = [](int k) { return (unsigned)(SSF::NF * WL) + (unsigned)k * (unsigned)RC_STRIDE; };
     const unsigned cold0 = (unsigned)(SSF::NF * WL) + (unsigned)RC_STRIDE * WL;
-    MR_LDS T* const LDX = lds + LDX_OFF;
-    const bool row = ln < NX;
-    const int li = row ? ln : 0;
-    // per-lane operand offsets: column li of A (vehicle rows: J[j][li], li < 6), column li of K, v_k[li];
-    // the shared J[j][6 + a] (B's vehicle rows) and u_k are the same address in every lane
-    unsigned aoff[6], koff[NU];
+    const int grp = ln >> 4, r = ln & 15;
+    const bool g0r = (grp == 0) & (r < NX), g1r = (grp == 1) & (r < NU);
+    const int li = g0r ? r : 0;
+    // per-lane gather plan: the coefficient column (E^ column r of A, or column 11 + r of B), K_k[0..2][r]
+    // (group 0), and the constant v_k[r] (group 0) / u_k[r] (group 1) from the cold fields
+    int coff[NX], koff[NU];
 #pragma unroll
-    for (int j = 0; j < 6; ++j) aoff[j] = li < 6 ? (unsigned)(RCF::J + j * 8 + li) : (unsigned)RCF::CZERO;
+    for (int j = 0; j < NX; ++j) coff[j] = g0r ? ehat_slot(j, r, true) : (g1r ? ehat_slot(j, NX + r, true) : RCF::CZERO);
 #pragma unroll
-    for (int a = 0; a < NU; ++a) koff[a] = (unsigned)(RCF::K + a * NX + li);
-    const int lr = ln < NU ? ln : 0;
-    const unsigned voff = (unsigned)(CSF::SPV + li) * WL, uoff = (unsigned)(CSF::SK0 + lr) * WL;
+    for (int a = 0; a < NU; ++a) koff[a] = g0r ? RCF::K + a * NX + r : RCF::CZERO;
+    const unsigned voff = g0r ? (unsigned)(CSF::SPV + r) * WL : (g1r ? (unsigned)(CSF::SK0 + r) * WL : (unsigned)CSF::SJUNK * WL);
     struct Ops {
-      T acol[6], kcol[NU], v, jb[12], u;
+      T c[NX], kc[NU], v;
     };
     auto ld = [&](int k, Ops& o) {
       const unsigned rk = (unsigned)wu(w, (int)R(k)), ck = (unsigned)wu(w, (int)(cold0 + (unsigned)k));
 #pragma unroll
-      for (int j = 0; j < 6; ++j) o.acol[j] = wb.ld(rk, aoff[j]);
+      for (int j = 0; j < NX; ++j) o.c[j] = wb.ld(rk, (unsigned)coff[j]);
 #pragma unroll
-      for (int a = 0; a < NU; ++a) o.kcol[a] = wb.ld(rk, koff[a]);
+      for (int a = 0; a < NU; ++a) o.kc[a] = wb.ld(rk, (unsigned)koff[a]);
       o.v = wb.ld(ck, voff);
-#pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        o.jb[2 * j] = wb.ld(rk, (unsigned)(RCF::J + j * 8 + 6));
-        o.jb[2 * j + 1] = wb.ld(rk, (unsigned)(RCF::J + j * 8 + 7));
-      }
-      o.u = wb.ld(ck, uoff);  // lane a < NU: u_k[a]
     };
     T pv = wb.ld((unsigned)wu(w, (int)(cold0 + (unsigned)N)), (unsigned)(CSF::SG + li) * WL);  // pv_N = g_x,N
-    LDX[row ? N * 12 + ln : LJUNK_OFF - LDX_OFF + ln] = pv;
     // the LDS base in a register (a member read after an LDS store is reloaded from the solver object,
-    // itself in LDS: one LDS round trip per step); r_k's slot (lanes < NU) or the lane's discard slot
+    // itself in LDS: one LDS round trip per step); group 0: LDX row k, group 1: r_k's slot, others: the
+    // lane's discard slot
     MR_LDS T* const LB = lds;
-    const int rbase = ln < NU ? LX_OFF + ln : LJUNK_OFF + ln, rstride = ln < NU ? 3 : 0;
+    const int pbase = g0r ? LDX_OFF + r : (g1r ? LX_OFF + r : LJUNK_OFF + ln), pstride = g0r ? 12 : (g1r ? 3 : 0);
+    if (g0r) lds[LDX_OFF + N * 12 + r] = pv;
     auto step = [&](int k, const Ops& o) {
       T p[NX];
       wgather<T, NX>(w, pv, p);
-      // B^T pv (mr_solver.h apply_Bt): every lane the same three values
-      T b0 = p[7], b1 = p[8], c0 = T(0), c1 = T(0);
-      if (k == 0) { b0 += p[9]; b1 += p[10]; }
+      T s0 = o.c[0] * p[0], s1 = o.c[1] * p[1];
 #pragma unroll
-      for (int j = 0; j < 6; j += 2) {
-        b0 += o.jb[2 * j] * p[j];
-        b1 += o.jb[2 * j + 1] * p[j];
-        c0 += o.jb[2 * j + 2] * p[j + 1];
-        c1 += o.jb[2 * j + 3] * p[j + 1];
+      for (int j = 2; j < NX; j += 2) {
+        s0 += o.c[j] * p[j];
+        if (j + 1 < NX) s1 += o.c[j + 1] * p[j + 1];
       }
-      b0 += c0;
-      b1 += c1;
-      const T b2 = p[6];
-      // (A^T pv)[li] (mr_solver.h apply_At): the vehicle columns from J, the structural ones selected
-      T at0 = o.acol[0] * p[0], at1 = o.acol[1] * p[1];
-      at0 += o.acol[2] * p[2];
-      at1 += o.acol[3] * p[3];
-      at0 += o.acol[4] * p[4];
-      at1 += o.acol[5] * p[5];
-      const T sx = ln == 6 ? p[6] : ((k > 0 && ln == 9) ? p[9] : ((k > 0 && ln == 10) ? p[10] : T(0)));
-      const T at = ln < 6 ? at0 + at1 : sx;
-      pv = o.v + at + o.kcol[0] * b0 + o.kcol[1] * b1 + o.kcol[2] * b2;
-      LDX[row ? k * 12 + ln : LJUNK_OFF - LDX_OFF + ln] = pv;
-      const T bt = lr == 0 ? b0 : (lr == 1 ? b1 : b2);
-      LB[rbase + rstride * k] = bt + o.u;  // r_k
+      const T sd = s0 + s1;  // group 0: (A^T pv)[r]; group 1: b[r] = (B^T pv)[r]
+      T pn = o.v + sd;       // group 1: r_k = b + u
+#pragma unroll
+      for (int a = 0; a < NU; ++a) pn += o.kc[a] * wbcast(w, sd, 16 + a);  // group 0: + K^T b (kc = 0 elsewhere)
+      pv = pn;
+      LB[pbase + pstride * k] = pn;
     };
     // operands two stages ahead, three rotating sets (unrolled by three: no register copies of in-flight
     // loads); a prefetch past stage 0 re-reads stage 0 (unconditional loads, exact waits).  Two ahead, not
-    // three: a wave has at most 63 vector-memory instructions outstanding (vmcnt), and 17 loads per stage
-    // x 4 sets exceeded it, stalling every prefetch's issue on the oldest load (tools/ubench/
-    // chain_loads_ubench.hip: 17 loads x 4 sets 969 cycles per stage, 11 x 4 271).  Scheduling barriers keep
+    // three: a wave has at most 63 vector-memory instructions outstanding (vmcnt).  Scheduling barriers keep
     // each prefetch ahead of the step it overlaps (left free, the scheduler sank the loads to the loop's end)
     if (N > 0) {
       auto kc = [](int k) { return k > 0 ? k : 0; };
@@ -2809,7 +2783,7 @@ struct WaveSolver {
   // res_alpha = a.
   MR_HD int soft_resto(T th, T ph, T gphi, T th_pow, T ap, T ad) {
     const T a = mr_min(ap, ad);
-    line_search<false, false>(th, ph, gphi, th_pow, a, a, a, 0, LS_FORCE, a, T(-1));
+    line_search<false, false>(th, ph, gphi, th_pow, a, a, a, 0, LS_FORCE, a);
     if (!(res_flags & LSR_FIN)) return 0;
     const T th_t = res_th, ph_t = res_ph;
     const LSRef<T> ref{th, ph, gphi, th_pow};
@@ -3012,7 +2986,7 @@ struct WaveSolver {
       T a_min = alpha_min_of(th, gphi);
       if (rs) {  // a restoration-phase step: its own filter, no watchdog, no second-order correction
         MR_T0();
-        line_search<true, false>(th, ph, gphi, th_pow, ap, ap, a_min, 0, 0, T(0), T(-1));
+        line_search<true, false>(th, ph, gphi, th_pow, ap, ap, a_min, 0, 0, T(0));
         MR_T1(3);
         MR_STAT((st_resto++, st_trials += res_ntr));
         if (!(res_flags & LSR_ACC)) { out.status = 3; break; }  // IPOPT: restoration failed
@@ -3081,13 +3055,12 @@ struct WaveSolver {
         }
         if (tiny) {  // IPOPT: a tiny step is taken without a line search (and, with small multiplier steps,
                      // forces a barrier decrease)
-          line_search<false, false>(th, ph, gphi, th_pow, ap, ap, ap, 0, LS_FORCE, ap, T(-1));
+          line_search<false, false>(th, ph, gphi, th_pow, ap, ap, ap, 0, LS_FORCE, ap);
           accepted = true;
           cw()->tiny = ysmall ? 1 : 0;
         } else if (wuni(w, cw()->in_wd != 0)) {
           auto* C = cw();
-          line_search<false, false>(C->wd_th, C->wd_ph, C->wd_gphi, C->wd_thpow, ap, ap, ap, 0, LS_WD, C->wd_ap,
-                                    T(-1));
+          line_search<false, false>(C->wd_th, C->wd_ph, C->wd_gphi, C->wd_thpow, ap, ap, ap, 0, LS_WD, C->wd_ap);
           flags = res_flags;
           rejf |= (flags & LSR_REJF) != 0;
           uth = C->wd_th;
@@ -3108,7 +3081,7 @@ struct WaveSolver {
             th_pow = C->wd_thpow;
             uth = th;
             uph = ph;
-            line_search<false, false>(th, ph, gphi, th_pow, T(0.5) * ap, ap, a_min, 1, LS_NOSOC, T(0), T(-1));
+            line_search<false, false>(th, ph, gphi, th_pow, T(0.5) * ap, ap, a_min, 1, LS_NOSOC, T(0));
             flags = res_flags;
             rejf |= (flags & LSR_REJF) != 0;
             accepted = (flags & LSR_ACC) != 0;
@@ -3120,7 +3093,7 @@ struct WaveSolver {
 #else
 #define MR_TQ(q) ((void)0)
 #endif
-          line_search<false, false>(th, ph, gphi, th_pow, ap, ap, a_min, 0, LS_CAP, T(0), T(-1));
+          line_search<false, false>(th, ph, gphi, th_pow, ap, ap, a_min, 0, LS_CAP, T(0));
           MR_TQ(16);
           flags = res_flags;
           rejf |= (flags & LSR_REJF) != 0;
@@ -3157,7 +3130,7 @@ struct WaveSolver {
               if (trace) tq = MR_CLOCK();
 #endif
               line_search<false, true>(th, ph, gphi, th_pow, aps, aps, aps, 0, LS_WD | LS_CAP,
-                                       a_test0, T(-1));
+                                       a_test0);
               MR_TQ(18);
               rejf |= (res_flags & LSR_REJF) != 0;
               a_soc = aps;
@@ -3175,7 +3148,7 @@ struct WaveSolver {
 #if MR_PHASE_CYCLES
               if (trace) { tsub[23] += 1; tq = MR_CLOCK(); }
 #endif
-              line_search<false, false>(th, ph, gphi, th_pow, T(0.5) * a_trial, ap, a_min, 1, LS_NOSOC, T(0), T(-1));
+              line_search<false, false>(th, ph, gphi, th_pow, T(0.5) * a_trial, ap, a_min, 1, LS_NOSOC, T(0));
               MR_TQ(20);
               flags = res_flags;
               rejf |= (flags & LSR_REJF) != 0;
