@@ -310,6 +310,34 @@ def pipelined(args, solver, dev_in, out, batch, B, dev, local, nstreams):
             "note": "independent batches in flight on separate streams (not the line's value)"}
 
 
+def shard_spread(args, solver, out, dev, stream, ms0):
+    """The other shards of the multi-GPU split solved one at a time on this GPU (N = 1 only; not the line's
+    value): the batch time is the slowest solve's latency, and which instances run to max_iter is decided by
+    rounding, so shard 0's time is one draw -- the 8-GPU job's time is the slowest shard's.  One warm launch per
+    shard, HIP events on the launch stream."""
+    import torch
+    from mpcracing import workload as wl
+    cfg = wl.CONFIGS[args.config]
+    per = args.per_gpu or cfg["per_gpu"]
+    n = max(1, cfg["B"] // per)
+    if n < 2:
+        return None
+    ms = [ms0]
+    for r in range(1, n):
+        b = wl.make_batch(args.config, rank=r, world=n, per_gpu=per)
+        d = solver.to_device(b)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        solver.launch(d, out, stream)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        ms.append(e0.elapsed_time(e1))
+    return {"shards": n, "ms_per_shard": [round(x, 2) for x in ms], "ms_max": round(max(ms), 2),
+            "ms_mean": round(float(np.mean(ms)), 2),
+            "note": "shard r of the 8-GPU split (workload.make_batch(config, r, 8)) on this GPU, one launch each "
+                    "(shard 0: the timed steps' p50); the 8-GPU job's batch time is the slowest shard's"}
+
+
 def cpu_check(args, rank, world):
     """--cpu-check: the multi-rank plumbing without a GPU (gloo): each rank builds its shard and the
     counters go through reduce_counters; rank 0 prints the shard layout.  Used by tests/test_multirank.py."""
@@ -457,6 +485,10 @@ def main():
     if args.pipeline >= 2 and world == 1 and not dry and not args.no_latency:
         pipe = pipelined(args, solver, dev_in, out, batch, B, dev, local, args.pipeline)
 
+    spread = None
+    if world == 1 and not dry and not args.no_latency:
+        spread = shard_spread(args, solver, out, dev, stream, float(np.median(kms)))
+
     tot, elapsed_max = reduce_counters(
         torch.tensor([B * args.steps, iters_launch, alg_bytes, B] + stc.tolist(), dtype=torch.float64, device=dev),
         elapsed, world)
@@ -521,6 +553,8 @@ def main():
         }
         if pipe is not None:
             line["pipelined"] = pipe
+        if spread is not None:
+            line["shard_spread"] = spread
         if agent is not None:
             line["agent_call"] = dict(agent, config=f"agent.py:154,171-183: B = 1, N = {AGENT_N}, dyn, fp64, "
                                                     f"Ts {AGENT_TS}, tol 1e-4 / acceptable 1e-2 x 15; the first 100 "
