@@ -239,7 +239,7 @@ def cpu_other_configs(budget_s):
     return res
 
 
-def reduce_counters(counts, elapsed, world):
+def reduce_counters(counts, elapsed, world, pg=False):
     """Whole-job totals over the ranks (the only collective of the run): SUM of the per-rank
     counters [solves, sum of iterations, algorithmic bytes, status histogram...] and MAX of the
     timed wall clock.  RCCL on the GPU box (backend "nccl"), gloo in the CPU tests."""
@@ -247,7 +247,7 @@ def reduce_counters(counts, elapsed, world):
     import torch.distributed as dist
     tot = counts.to(torch.float64)
     tmax = torch.tensor([float(elapsed)], dtype=torch.float64, device=tot.device)
-    if world > 1:
+    if world > 1 or pg:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     return tot.cpu().numpy(), float(tmax.item())
@@ -405,8 +405,12 @@ def main():
     dry = args.dry_run
     if dry and backend != "gloo":
         raise SystemExit("--dry-run needs MR_BENCH_BACKEND=gloo (it is the CPU test of the rank plumbing)")
-    if world > 1:
+    # MR_BENCH_PG=1: the process group and its collectives also at world size 1 -- the multi-GPU path's RCCL
+    # initialisation (device_id), barriers and counter all-reduce exercised on a one-GPU box
+    pg = world > 1 or os.environ.get("MR_BENCH_PG") == "1"
+    if pg:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
         if dry:
             dist.init_process_group(backend, rank=rank, world_size=world)
         else:
@@ -421,10 +425,10 @@ def main():
     B = int(batch["s0"].shape[0])
     W = 4 if cfg["precision"] == "fp32" else 8
     if dry:  # no solve: zero iterations, every instance "solved", unit timings
-        if world > 1:
+        if pg:
             dist.barrier()
         t0 = time.perf_counter()
-        if world > 1:
+        if pg:
             dist.barrier()
         elapsed = time.perf_counter() - t0
         kms = [1.0] * args.steps
@@ -442,7 +446,7 @@ def main():
 
         starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
         ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-        if world > 1:
+        if pg:
             dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
@@ -451,7 +455,7 @@ def main():
             solver.launch(dev_in, out, stream)
             ends[s].record(stream)
         torch.cuda.synchronize(dev)
-        if world > 1:
+        if pg:
             dist.barrier()
         elapsed = time.perf_counter() - t0
         # per-launch kernel durations (HIP events on the launch stream)
@@ -491,7 +495,7 @@ def main():
 
     tot, elapsed_max = reduce_counters(
         torch.tensor([B * args.steps, iters_launch, alg_bytes, B] + stc.tolist(), dtype=torch.float64, device=dev),
-        elapsed, world)
+        elapsed, world, pg)
 
     copy_gbs = None
     if rank == 0 and not dry:
@@ -561,10 +565,14 @@ def main():
                                                     "C2 instances (cpu side: cpu_baseline.agent_call_1thread_ms)")
         if dry:
             line["dry_run"] = True
+        if pg:
+            line["process_group"] = {"backend": dist.get_backend(), "world_size": world,
+                                     "collectives": "barrier around the timed steps; all_reduce SUM of the counters, "
+                                                    "MAX of the wall clock"}
         if world == 1 and not args.no_cpu_baseline and not dry:
             line["cpu_baseline"] = cpu_baseline(args.config, batch, it, args.cpu_budget)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if pg:
         dist.destroy_process_group()
 
 
