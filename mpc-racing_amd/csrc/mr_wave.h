@@ -1697,13 +1697,14 @@ struct WaveSolver {
       dv[j] = SOCDIR ? Cf(CSF::SDS + j) : S(SSF::DS + j);
     }
     unsigned actm = 0u;  // active rows of this stage (depend on the stage only, not on the point)
+    T rlo[NROW], rhi[NROW];  // their bounds, once per line search (row_values recomputed them per trial)
 #pragma unroll
     for (int r = 0; r < NROW; ++r) {
       int a;
-      T lo, hi;
-      row_bounds(P, I, k, r, a, lo, hi);
+      row_bounds(P, I, k, r, a, rlo[r], rhi[r]);
       actm |= (own() && a) ? (3u << (2 * r)) : 0u;
     }
+    const T lmax = I.max_err + relax_amt(I.max_err);  // the lane rows' relaxed bound (lane_d)
     actm |= (own() && lane_active(P, k)) ? (3u << JL) : 0u;
     for (int j = 0; j < NI; ++j) {
       const bool a = (actm >> j) & 1u;
@@ -1760,9 +1761,16 @@ struct WaveSolver {
       if (own()) {
         Err<T> e;
         errors(I, zt[0], zt[1], zt[6], e, false);
-        T d[NI];
-        int act[NI];
-        row_values(k, zt, e, d, act);
+        T d[NI];  // row_values with the line search's bounds (the same values; activity from actm)
+#pragma unroll
+        for (int r = 0; r < NROW; ++r) {
+          const T c = row_c(r, zt);
+          d[2 * r] = c - rlo[r];
+          d[2 * r + 1] = rhi[r] - c;
+        }
+        d[JL] = e.eC + lmax + T(0);
+        d[JL + 1] = lmax - e.eC + T(0);
+        d[JL + 2] = T(0);
         if constexpr (!RESTO) {
           // branch-free over the slots (the per-slot activity test compiled to a divergent branch each):
           // an inactive slot has s = 1, ds = 0 (setup above), so s + alpha ds = 1 > 0 and log 1 = 0 add
