@@ -114,6 +114,18 @@ __global__ __launch_bounds__(WL, sizeof(T) == 4 ? MR_WAVES_PER_SIMD_F32 : MR_WAV
   __shared__ alignas(16) char slots[WL * sizeof(WaveSolver<T, MODEL, SSL>)];
   __shared__ WaveShared<T> wsh;  // the line-search filter and the watchdog / restoration state, shared by the wave
   T* const filt_sh = wsh.filt;
+#ifdef MR_POISON
+  {  // developer check (tools/determinism_probe.py): LDS and the instance's workspace start as a fixed pattern,
+     // 1 NaN / 2 zero / 3 -1e30, so a read before the solve's first write shows as a difference between patterns
+    const T pv = MR_POISON == 1 ? (T)NAN : MR_POISON == 2 ? T(0) : T(-1e30);
+    for (int q = threadIdx.x; q < LDS_WORDS; q += WL) lds[q] = pv;
+    for (int q = threadIdx.x; q < (int)(sizeof(slots) / sizeof(T)); q += WL) ((T*)slots)[q] = pv;
+    for (int q = threadIdx.x; q < (int)(sizeof(wsh) / sizeof(T)); q += WL) ((T*)&wsh)[q] = pv;
+    for (int q = threadIdx.x; q < (int)(sizeof(Ish) / sizeof(T)); q += WL) ((T*)&Ish)[q] = pv;
+    for (int64_t q = threadIdx.x; q < ws_words<T>(); q += WL) wsi[q] = pv;
+    __syncthreads();
+  }
+#endif
   if constexpr (SSL) {
     __shared__ T ssl[SS_WORDS];
     solve_instance_wave<T, MODEL, true, true>(P, in, out, B, i, wsi, (MR_LDS T*)lds, w, (MR_LDS T*)ssl, &Ish,

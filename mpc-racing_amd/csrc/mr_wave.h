@@ -136,7 +136,10 @@ struct CSF {
 // Riccati right-hand side from them in fp64 (the correction form, see there).
 constexpr int64_t WS_NU_OFF = (int64_t)SSF::NF * WL + (int64_t)RC_STRIDE * WL + (int64_t)CSF::NF * WL;  // words
 template <typename T>
-MR_HD constexpr int64_t ws_words() { return WS_NU_OFF + 3 * NX * WL * (int64_t)(sizeof(double) / sizeof(T)); }
+#ifndef MR_WS_PAD
+#define MR_WS_PAD 0  // developer check (tools/build_flag_variants.py wspad): unused words after each instance's workspace
+#endif
+MR_HD constexpr int64_t ws_words() { return WS_NU_OFF + 3 * NX * WL * (int64_t)(sizeof(double) / sizeof(T)) + MR_WS_PAD; }
 
 // Wave-uniform state of the watchdog and the restoration phase: one copy per wavefront next to the
 // line-search filter (LDS on the device), every lane writing the same values -- not in the per-lane
@@ -1742,11 +1745,12 @@ struct WaveSolver {
     T zt[NZS], st[NI];
     const T kdm = T(IP_KAPPA_D) * mu;
     // one trial point: zt, st (registers), theta, phi; false if a slack is not positive or a value is
-    // not finite.  CAP (compile-time: std::true_type / false_type): also write its constraint values to the
-    // cold fields CTR / CTC for a second-order correction (LS_CAP) -- two instantiations, so the regular
-    // trials carry no per-slot store branches
-    auto eval = [&](T alpha, T& th_t, T& ph_t, auto CAPT) -> bool {
-      constexpr bool cap = decltype(CAPT)::value;
+    // not finite.  cap: also write its constraint values to the cold fields CTR / CTC for a second-order
+    // correction (LS_CAP).  One body with a run-time flag: the form with two compile-time instantiations
+    // selected by (capm && n == 0) -- a branch the compiler must treat as divergent, mode being a VGPR
+    // argument -- made the fp64 C5 solves differ from run to run in the second-order-correction steps
+    // (tools/determinism_probe.py; bisected to that change); this form is bit-identical run to run
+    auto eval = [&](T alpha, T& th_t, T& ph_t, bool cap) -> bool {
 #if MR_PHASE_CYCLES
       const unsigned long long te0 = trace ? MR_CLOCK() : 0ull;
 #endif
@@ -1786,8 +1790,8 @@ struct WaveSolver {
             if (yslot(j)) {
               const T r = d[j] - sj;
               th_l += a ? mr_abs(r) : T(0);
-              if constexpr (cap) Cf(CSF::CTR + j) = a ? T(slot_sign(j)) * r : T(0);
-            } else if constexpr (cap) {
+              if (cap) Cf(CSF::CTR + j) = a ? T(slot_sign(j)) * r : T(0);
+            } else if (cap) {
               Cf(CSF::CTR + j) = T(0);
             }
           }
@@ -1835,10 +1839,10 @@ struct WaveSolver {
           } else {
             for (int i = 0; i < NX; ++i) {
               th_l += mr_abs(xn[i] - ztn[i]);
-              if constexpr (cap) Cf(CSF::CTC + i) = xn[i] - ztn[i];
+              if (cap) Cf(CSF::CTC + i) = xn[i] - ztn[i];
             }
           }
-        } else if constexpr (!RESTO && cap) {
+        } else if (!RESTO && cap) {
           for (int i = 0; i < NX; ++i) Cf(CSF::CTC + i) = T(0);
         }
       }
@@ -1881,7 +1885,7 @@ struct WaveSolver {
     bool store = false;
     if (mode & LS_FORCE) {
       alpha = a_fix;
-      const bool fin = eval(alpha, th_t, ph_t, std::false_type{});
+      const bool fin = eval(alpha, th_t, ph_t, false);
       ntr++;
       flags |= fin ? LSR_FIN : 0;
       store = true;
@@ -1891,8 +1895,7 @@ struct WaveSolver {
       for (int n = 0; n < IP_LS_MAX; ++n) {
         if (!(alpha > a_min || n == 0)) break;
         a_test = (mode & LS_WD) ? a_fix : alpha;
-        const bool fin = (capm && n == 0) ? eval(alpha, th_t, ph_t, std::true_type{})
-                                          : eval(alpha, th_t, ph_t, std::false_type{});
+        const bool fin = eval(alpha, th_t, ph_t, capm && n == 0);
         ntr++;
 #if MR_PHASE_CYCLES
         const unsigned long long ta0 = trace ? MR_CLOCK() : 0ull;
