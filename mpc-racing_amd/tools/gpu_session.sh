@@ -8,6 +8,8 @@
 #   phase   tools/phase_probe.py on the C4 tail instances (cycle-counter build in variants/)
 #   tl      tools/timeline_probe.py C4
 #   c2 c3 c5  bench.py --config Cx --no-cpu-baseline
+#   agent   tools/agent_probe.py (the B = 1 agent call alone)
+#   agent_ic  the same under one PMC pass: instruction-cache hits / misses and wave wait cycles
 # Usage: gpu_session.sh TAG step...
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
@@ -31,6 +33,8 @@ for s in "$@"; do
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-latency ;;
     phase) step phase 600 env MR_PRODUCT_LIB=variants/lib_cycles.so python -u mpc-racing_amd/tools/phase_probe.py C4 ;;
     tl) step tl 300 python -u mpc-racing_amd/tools/timeline_probe.py C4 1 ;;
+    agent) step agent 300 python -u mpc-racing_amd/tools/agent_probe.py 100 ;;
+    agent_ic) step agent_ic 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQC_ICACHE_HITS SQC_ICACHE_MISSES -d gpurun_out/${TAG}_agent_ic -o run --output-format csv -- python -u mpc-racing_amd/tools/agent_probe.py 10 ;;
     c2|c3|c5) C=$(echo $s | tr a-z A-Z); step bench_$C 600 python bench.py --config $C --no-cpu-baseline ;;
     *) echo "unknown step $s" >> gpurun_out/${TAG}_session.log ;;
   esac
