@@ -7,6 +7,7 @@ bounds of mpcracing.hip): variants/lib_<name>.so, run by tools/gpu_flags_ab.sh o
   w1       fp32 solve kernel at 1 wave per SIMD (MR_WAVES_PER_SIMD_F32=1, 512 VGPRs)
   cyc      per-sweep shader-cycle counters of the trace instance (tools/phase_probe.py)
   nofma    no floating-point contraction (-ffp-contract=off: the host build's arithmetic, no FMA)
+  inline   the sweeps force-inlined into the solve kernel (MR_SWEEP_INLINE: one register allocation, no call ABI)
   wspad    64 Ki unused words after each instance's workspace (an out-of-range write would land there)
   poisonP  LDS and workspace filled with pattern P (1 NaN, 2 zero, 3 -1e30) at kernel start (determinism_probe.py)
 """
@@ -29,6 +30,7 @@ VARIANTS = {
     "poison1": DEFAULT_FLAGS + ["-DMR_POISON=1"],
     "poison2": DEFAULT_FLAGS + ["-DMR_POISON=2"],
     "poison3": DEFAULT_FLAGS + ["-DMR_POISON=3"],
+    "inline": DEFAULT_FLAGS + ["-DMR_SWEEP_INLINE=1"],
     "wspad": DEFAULT_FLAGS + ["-DMR_WS_PAD=65536"],
 }
 
